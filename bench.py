@@ -1,0 +1,201 @@
+"""bench.py - graph edges/s through the CSR SpMM at d=64 on MI355X.
+
+Workload (BASELINE.json north_star): synthetic bipartite graph, 10M users x
+1M items, 200M uniform (user, item) draws (seed 0), symmetric D^-1/2 A D^-1/2
+values built exactly as utils.generate_daj_mat + LightGCN.generate_graph,
+X ~ N(0, 0.1^2).  One step = one graph-convolution layer Y = A X over every
+edge of the graph (model.py:4196 / 106): the user-side SpMM, the item-side
+SpMM and, for N > 1, the RCCL all-reduce of the item partials (igr.dist).
+Inputs are resident in HBM before the timed region.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 via
+torch.distributed.run (one process per GPU, RCCL over xGMI).  Rank 0 prints
+ONE JSON line.  The CPU baseline (rank 0, N = 1 only) times the oracle's C
+OpenMP SpMM - a restatement of DGL's CPU SpMMSumCsr - on a bounded sample of
+the same graph.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'inductive-recommendation_amd'))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = 'graph edges/sec through SpMM at d=64'
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(f'[bench {time.strftime("%H:%M:%S")}]', *a, file=sys.stderr, flush=True)
+
+
+def spmm_bytes(nnz, n_rows, d):
+    """Algorithmic bytes of one SpMM launch: int32 col + fp32 val
+    + one gathered fp32 source row per edge; int64 row_ptr + one output row per row."""
+    return nnz * (4 + 4 + 4 * d) + n_rows * (8 + 4 * d)
+
+
+def cpu_baseline(shard, x_users, x_items, d, seconds, sample_edges):
+    """Oracle C SpMM (OpenMP) on the first rows of both blocks, ~sample_edges edges."""
+    from oracle import igr_oracle as O
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
+    lib = O.lib()
+    parts = []
+    for blk, vals, lhs in [(shard.user_block, shard.user_vals, x_items), (shard.item_block, shard.item_vals, x_users)]:
+        h = blk.host()
+        rp = h['row_ptr']
+        R = int(min(np.searchsorted(rp, sample_edges // 2), blk.n_rows))
+        e = int(rp[R])
+        parts.append((R, np.ascontiguousarray(rp[:R + 1]), h['col_idx'][:e].astype(np.int64),
+                      vals[:e].cpu().numpy(), lhs.cpu().numpy()))
+    edges = sum(int(p[1][-1]) for p in parts)
+    outs = [np.empty((p[0], d), np.float32) for p in parts]
+    iters, t0 = 0, time.perf_counter()
+    while True:
+        for (R, rp, ci, v, x), out in zip(parts, outs):
+            lib.orc_spmm_sum_f32(R, d, rp, ci, v, None, x, d, out, d, threads)
+        iters += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {'value': edges * iters / el, 'unit': 'edges/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{edges} edges (first {parts[0][0]} user rows + first {parts[1][0]} item rows of the same '
+                      f'graph), d={d}, {iters} passes in {el:.1f}s, oracle/oracle.c orc_spmm_sum_f32 '
+                      f'(restated DGL CPU SpMMSumCsr, gcc -O2 -fopenmp)'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--n-users', type=int, default=10_000_000)
+    ap.add_argument('--n-items', type=int, default=1_000_000)
+    ap.add_argument('--n-edges', type=int, default=200_000_000)
+    ap.add_argument('--d', type=int, default=64)
+    ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--item-dist', default='uniform', choices=['uniform', 'zipf'])
+    ap.add_argument('--cpu-seconds', type=float, default=15.0, help='CPU baseline budget (0 = skip)')
+    ap.add_argument('--cpu-sample-edges', type=int, default=20_000_000)
+    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'))
+    args = ap.parse_args()
+
+    rank = int(os.environ.get('RANK', 0))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    local_rank = int(os.environ.get('LOCAL_RANK', 0))
+    assert world == args.gpus, f'--gpus {args.gpus} but WORLD_SIZE={world}'
+    torch.cuda.set_device(local_rank)
+    dev = torch.device('cuda', local_rank)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)  # RCCL over xGMI
+
+    from igr import ops
+    from igr.dataset import synthetic_pairs
+    from igr.dist import BipartiteShard
+
+    U, I, E, d = args.n_users, args.n_items, args.n_edges, args.d
+    t0 = time.time()
+    log(f'rank {rank}/{world}: drawing {E} interactions (U={U}, I={I}, {args.item_dist}, seed {args.seed})')
+    pairs = synthetic_pairs(U, I, E, args.seed, args.item_dist)
+    log(f'building shard (C++ CSR build) ... {time.time() - t0:.1f}s')
+    shard = BipartiteShard(pairs, U, I, rank, world, dev)
+    del pairs
+    nu = shard.u1 - shard.u0
+    log(f'shard users [{shard.u0}, {shard.u1}) local nnz {shard.local_nnz} '
+        f'(user block {shard.user_block}, item block {shard.item_block}) ... {time.time() - t0:.1f}s')
+
+    g = torch.Generator(device=dev).manual_seed(2 + args.seed)
+    x_items = torch.randn(I, d, generator=g, device=dev) * 0.1
+    g.manual_seed(3 + args.seed + rank)
+    x_users = torch.randn(nu, d, generator=g, device=dev) * 0.1
+    y_users = torch.empty(nu, d, device=dev)
+    y_items = torch.empty(I, d, device=dev)
+    stream = torch.cuda.current_stream()
+    blocks = [(shard.item_block, shard.item_vals, x_users, y_items), (shard.user_block, shard.user_vals, x_items, y_users)]
+    launch_bytes = [spmm_bytes(b.nnz, b.n_rows, d) for b, _, _, _ in blocks]
+
+    def step(events=None):
+        for k, (blk, vals, x, y) in enumerate(blocks):
+            if events is not None:
+                events[k][0].record(stream)
+            ops.spmm(blk, x, vals, out=y)
+            if events is not None:
+                events[k][1].record(stream)
+            if k == 0 and world > 1:
+                work = dist.all_reduce(y_items, op=dist.ReduceOp.SUM, async_op=True)
+        if world > 1:
+            work.wait()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [[[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(2)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for s in range(args.steps):
+        step(ev[s])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kern_ms = np.array([[ev[s][k][0].elapsed_time(ev[s][k][1]) for k in range(2)] for s in range(args.steps)])
+
+    stats = torch.tensor([elapsed, float(shard.local_nnz)], dtype=torch.float64, device=dev)
+    if world > 1:
+        t = stats[:1].clone()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n = stats[1:].clone()
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        elapsed, total_nnz = float(t.item()), int(n.item())
+    else:
+        total_nnz = shard.local_nnz
+    value = total_nnz * args.steps / elapsed
+    avg_kernel_s = float(kern_ms.mean()) / 1e3
+    avg_bytes = float(np.mean(launch_bytes))
+    achieved = avg_bytes / avg_kernel_s / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        key = f'd{d}_U{U}_I{I}_E{E}_w{world}'
+        traffic = tj.get(key, {}).get('hbm_bytes_per_launch')
+    log(f'elapsed {elapsed:.4f}s for {args.steps} steps; kernel avg {avg_kernel_s * 1e3:.3f} ms '
+        f'(user {kern_ms[:, 1].mean():.3f} ms, item {kern_ms[:, 0].mean():.3f} ms); {achieved:.0f} GB/s algorithmic')
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        log('CPU baseline ...')
+        cpu = cpu_baseline(shard, x_users, x_items, d, args.cpu_seconds, args.cpu_sample_edges)
+        log(f'CPU baseline {cpu["value"] / 1e9:.3f} G edges/s on {cpu["cores"]} threads')
+
+    if rank == 0:
+        out = {
+            'metric': METRIC, 'value': value, 'unit': 'edges/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': elapsed / args.steps * 1e3, 'higher_is_better': True,
+            'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+            'config': {'workload': f'synthetic bipartite {U} users x {I} items, {E} {args.item_dist} draws, '
+                                   f'd={d}: one SpMM layer Y = D^-1/2 A D^-1/2 X over all {total_nnz} edges',
+                       'n_users': U, 'n_items': I, 'n_draws': E, 'nnz': total_nnz, 'd': d,
+                       'parallelism': f'user-range shards x{world}, item block replicated, RCCL all-reduce'},
+            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
+                         'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic,
+                         'kernel': 'igr::spmm_main<64,true,false>',
+                         'avg_launch_ms': avg_kernel_s * 1e3, 'algorithmic_bytes_per_launch': avg_bytes},
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,213 @@
+/*
+ * igr.h - C-ABI of the MI355X (gfx950) inductive graph-convolution path.
+ *
+ * Drop-in boundary for the DGL operator API the reference sits on
+ * (SURVEY.md §8b).  The reference binds, from Python:
+ *     g = dgl.graph((column, row), num_nodes=n, device=dev)      model.py:103-105, 4183, 4194
+ *     dgl.ops.gspmm(g, 'mul', 'sum', lhs_data=X, rhs_data=vals)  model.py:106, 4184, 4196, 4037
+ *     dgl.ops.gspmm(g, 'copy_rhs', 'max'|'sum', None, alpha)     model.py:4270, 4273 (AttIGCN)
+ *     AttIGCN.masked_mm (index_select x2 + mul + sum)             model.py:4246-4255
+ *     rep[users], rep[n_users + pos/neg] (BPR gathers)            model.py:4048-4049
+ * Every entry point below replaces one of those; the ctypes binding that
+ * calls them is inductive-recommendation_amd/igr/_lib.py.
+ *
+ * Conventions
+ *  - Plain pointers and sizes.  Device pointers are HIP device memory
+ *    allocated by the CALLER (PyTorch); this library never allocates, frees
+ *    or synchronises inside a device entry point (graph-capture safe).
+ *  - `stream` is a hipStream_t passed as void*; work is enqueued on it.
+ *  - Return 0 on success, a non-zero IGR_ERR_* code otherwise; the message
+ *    is in igr_last_error() (thread-local).  No C++ exception crosses the ABI.
+ *  - Graph convention as in the reference: rows = destination nodes (DGL
+ *    dst = `row`), columns = source nodes (DGL src = `column`).  Edge data
+ *    (`rhs`) is indexed by EDGE ID; edge id = CSR position unless the graph
+ *    carries an `edge_id` permutation (multigraph built from unsorted COO).
+ *  - fp32 throughout (the reference computes in float32).
+ */
+#ifndef IGR_H
+#define IGR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IGR_OK 0
+#define IGR_ERR_ARG 1
+#define IGR_ERR_HIP 2
+#define IGR_ERR_UNSUPPORTED 3
+#define IGR_ERR_INTERNAL 4
+
+/* A CSR graph resident in device memory plus its row schedule.
+ * Built once per graph by the host functions below (the reference rebuilds
+ * a dgl.graph on every call, model.py:4183/4194; the values may change per
+ * step, the structure never does). */
+typedef struct igr_csr {
+    int64_t n_rows;             /* destination nodes                              */
+    int64_t n_cols;             /* source nodes (rows of lhs)                     */
+    int64_t nnz;
+    const int64_t *row_ptr;     /* [n_rows + 1]                                   */
+    const int32_t *col_idx;     /* [nnz], sorted within each row                  */
+    const int64_t *edge_id;     /* [nnz] CSR position -> edge id, or NULL (=id)   */
+    /* schedule (igr_plan_fill): rows with degree <= split_threshold are
+     * processed one per lane-group, heaviest first; longer rows are cut into
+     * chunks of chunk_edges edges whose partial sums are combined in order
+     * (deterministic, no atomics). */
+    int64_t n_order;
+    const int32_t *order;       /* [n_order] row ids                              */
+    int64_t n_split;
+    const int32_t *split_row;   /* [n_split] row ids                              */
+    const int64_t *split_ptr;   /* [n_split + 1] chunk ranges                     */
+    int64_t n_chunks;
+    const int32_t *chunk_row;   /* [n_chunks]                                     */
+    const int64_t *chunk_beg;   /* [n_chunks] first CSR position of the chunk     */
+    int64_t chunk_edges;
+} igr_csr;
+
+/* Fused row epilogue of a SpMM:
+ *   y[r]   = alpha * (A x)[r] + beta * add[r]            (add may be NULL)
+ *   acc_mode 1: acc[r] = y[r] / acc_div
+ *   acc_mode 2: acc[r] = (acc[r] + y[r]) / acc_div
+ * It fuses the layer-mean of LightGCN/IGCN get_rep (model.py:108-109,
+ * 4198-4199) and the "+ g/(L+1)" of its backward into the SpMM. */
+typedef struct igr_epilogue {
+    float alpha;
+    float beta;
+    const float *add;
+    int64_t ld_add;
+    float *acc;
+    int64_t ld_acc;
+    int32_t acc_mode;
+    float acc_div;
+    int32_t skip_y;             /* 1: do not store y                             */
+} igr_epilogue;
+
+/* ------------------------------------------------------------------ misc */
+const char *igr_last_error(void);
+int igr_version(void);
+/* Device properties used by the host side (CU count, L2, arch name). */
+int igr_device_info(int device, int *n_cu, int *l2_bytes, char *arch, int arch_len);
+
+/* ------------------------------------------------------- host graph build
+ * Host (CPU) functions on host memory; multi-threaded (n_threads <= 0: all).
+ * They replace the reference's Python/scipy construction
+ * (utils.py:33-50, model.py:89-98, model.py:4139-4175). */
+
+/* COO -> CSR sorted by (row, col).  dedup=1 sums duplicate (row, col)
+ * entries (scipy .tocsr() + torch .coalesce(), utils.py:38, 47-49); dedup=0
+ * keeps every edge (DGL multigraph) and records edge_id.  Output arrays hold
+ * `nnz` entries; *nnz_out receives the stored count.  val/edge_id nullable. */
+int igr_csr_from_coo(int64_t n_rows, int64_t n_cols, int64_t nnz, const int64_t *row,
+                     const int64_t *col, const float *val, int32_t dedup, int64_t *row_ptr,
+                     int32_t *col_idx, float *val_out, int64_t *edge_id, int64_t *nnz_out,
+                     int32_t n_threads);
+
+/* Transposed CSR (reverse graph for the gspmm backward):
+ * t_row_ptr [n_cols+1], t_col_idx [nnz] (= source row), t_pos [nnz] = CSR
+ * position in the forward graph of each transposed entry. */
+int igr_csr_transpose(int64_t n_rows, int64_t n_cols, const int64_t *row_ptr,
+                      const int32_t *col_idx, int64_t *t_row_ptr, int32_t *t_col_idx,
+                      int64_t *t_pos, int32_t n_threads);
+
+/* Row sums of a CSR's values (degree when the values are 1; exact in fp32
+ * below 2^24).  val NULL means 1. */
+int igr_csr_row_sums(int64_t n_rows, const int64_t *row_ptr, const float *val, float *out);
+
+/* Symmetric normalisation values (model.py:91-96):
+ *   out[p] = (dinv_row[r] * val[p]) * dinv_col[col[p]]
+ * dinv_col = dinv_row for the square adjacency; distinct for a rectangular
+ * user x item block of a sharded graph.  val NULL means 1. */
+int igr_sym_norm_values(int64_t n_rows, const int64_t *row_ptr, const int32_t *col_idx,
+                        const float *val, const float *dinv_row, const float *dinv_col, float *out);
+
+/* Row schedule.  igr_plan_size returns the array sizes, igr_plan_fill fills
+ * host arrays that the caller copies to the device and references from
+ * igr_csr. */
+int igr_plan_size(int64_t n_rows, const int64_t *row_ptr, int64_t split_threshold,
+                  int64_t chunk_edges, int64_t *n_order, int64_t *n_split, int64_t *n_chunks);
+int igr_plan_fill(int64_t n_rows, const int64_t *row_ptr, int64_t split_threshold,
+                  int64_t chunk_edges, int32_t *order, int32_t *split_row, int64_t *split_ptr,
+                  int32_t *chunk_row, int64_t *chunk_beg);
+
+/* ------------------------------------------------------- device kernels */
+
+/* gspmm(g, 'mul', 'sum', lhs_data=x, rhs_data=rhs) - CSR SpMM, fp32.
+ * Replaces dgl.ops.gspmm at model.py:106, 4184, 4196, 4037 (and its
+ * reverse-graph backward).  x: [n_cols, d] with leading dim ldx; rhs: edge
+ * weights by edge id (NULL = 1); y: [n_rows, d] with leading dim ldy.
+ * workspace: n_chunks * d floats (NULL allowed when n_chunks == 0).
+ * epi may be NULL (plain y = A x). */
+int igr_spmm_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx, const float *rhs,
+                 float *y, int64_t ldy, const igr_epilogue *epi, float *workspace, void *stream);
+
+/* u_dot_v SDDMM: out[eid(p), h] = <u[row_p, h, :], v[col_p, h, :]>.
+ * AttIGCN.masked_mm (model.py:4246-4255) with u = x_q (dst rows),
+ * v = x_k (src rows); with h = 1 it is also the gspmm rhs-gradient.
+ * u: [n_rows, h*d] (ld_u), v: [n_cols, h*d] (ld_v), out: [nnz, h]. */
+int igr_sddmm_dot_f32(const igr_csr *g, int32_t h, int32_t d, const float *u, int64_t ld_u,
+                      const float *v, int64_t ld_v, float *out, void *stream);
+
+/* gspmm(g, 'copy_rhs', 'sum'|'max', None, x): out[r, h] = reduce over edges
+ * of row r of x[eid, h]; empty rows give 0 (model.py:4270, 4273).
+ * reduce: 0 = sum, 1 = max. */
+int igr_segment_reduce_f32(const igr_csr *g, int32_t h, const float *x, int32_t reduce,
+                           float *out, void *stream);
+
+/* AttIGCN edge softmax, model.py:4270-4275, fused:
+ *   m = segmax(alpha); a = exp((alpha - m[row]) / sqrt_d / 10); s = segsum(a);
+ *   w[eid] = mean_h a / s[row]
+ * row_max / row_sum ([n_rows, h]) are saved for the backward. */
+int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alpha, float sqrt_d, float *w,
+                        float *row_max, float *row_sum, void *stream);
+/* Backward of igr_att_softmax_f32: dalpha[eid, h] from dw[eid]. */
+int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float *alpha, float sqrt_d,
+                            const float *row_max, const float *row_sum, const float *dw,
+                            float *dalpha, void *stream);
+
+/* NGCF.dropout_sp_mat (model.py:4016-4028) as a value mask over the fixed
+ * CSR: out = floor((1-p) + rand) ? val / (1-p) : 0.  rand ~ U[0,1), [n]. */
+int igr_edge_dropout_f32(int64_t n, const float *val, const float *rand, float p, float *out,
+                         void *stream);
+
+/* IGCN.update_feat_mat (model.py:4127-4130): out[p] = row_sum[row_p] ^ exponent,
+ * exponent = (alpha - 1)/2 - 0.5 (= 1/sqrt for alpha = 1). */
+int igr_feat_values_f32(int64_t n_rows, const int64_t *row_ptr, const float *row_sum,
+                        float exponent, float *out, void *stream);
+
+/* Row gather: out[i, :] = src[idx[i] + offset, :]  (rep[users], rep[n_users + pos],
+ * model.py:4048-4049; Embedding lookups trainer.py:544-546). */
+int igr_gather_rows_f32(int64_t n, int32_t d, const int64_t *idx, int64_t offset,
+                        const float *src, int64_t ld_src, float *out, int64_t ld_out, void *stream);
+/* Row scatter-add (gather backward): dst[idx[i] + offset, :] += src[i, :] (float atomics). */
+int igr_scatter_add_rows_f32(int64_t n, int32_t d, const int64_t *idx, int64_t offset,
+                             const float *src, int64_t ld_src, float *dst, int64_t ld_dst,
+                             void *stream);
+
+/* Fused BPR step terms (model.py:4046-4052 + trainer.py:536-540, 542-548):
+ * for each sample b: u = t[off_u + users[b]], p = t[off_i + pos[b]], n = t[off_i + neg[b]]
+ *   s_b = sum_k u_k (n_k - p_k) * (w ? w_k : 1)
+ *   loss[b] = softplus(s_b);  l2[b] = |u|^2 + |p|^2 + |n|^2      (loss/l2 nullable)
+ * and, if grad != NULL, accumulates  g_loss * dloss_b/dt + g_l2 * dl2_b/dt
+ * into grad (float atomics); if dw != NULL, g_loss * dloss_b/dw into dw.
+ * (g_loss = dL/dloss_b, e.g. 1/batch for a mean.) */
+int igr_bpr_fwd_bwd_f32(int64_t batch, int32_t d, const int64_t *users, const int64_t *pos,
+                        const int64_t *neg, int64_t off_u, int64_t off_i, const float *t,
+                        int64_t ld_t, const float *w, float *loss, float *l2, float g_loss,
+                        float g_l2, float *grad, int64_t ld_grad, float *dw, void *stream);
+
+/* Dense fp32 GEMM on MFMA (v_mfma_f32_16x16x4_f32, exact fp32 products):
+ *   C[m, n] = sum_k A(m, k) * B(k, n) + bias[n]
+ * A(m, k) = a[m*lda + k] (trans_a = 0) or a[k*lda + m] (trans_a = 1);
+ * B(k, n) = b[n*ldb + k] (trans_b = 0: nn.Linear weight [N, K]) or
+ *           b[k*ldb + n] (trans_b = 1).  bias nullable.
+ * The d x d / d x 4d projections of NGCF (model.py:4039) and AttIGCN
+ * (model.py:4259, 4264), forward and backward. */
+int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int64_t lda, int32_t trans_a,
+                 const float *b, int64_t ldb, int32_t trans_b, const float *bias, float *c,
+                 int64_t ldc, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IGR_H */

@@ -1,0 +1,87 @@
+// common.h - shared helpers for the igr HIP library (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <exception>
+#include <string>
+
+#include "igr.h"
+
+namespace igr {
+
+void set_error(const std::string &msg);
+
+// Run `body`, converting exceptions to an error code (no exception crosses the C ABI).
+template <class F>
+int guarded(const char *fn, F &&body) {
+    try {
+        return body();
+    } catch (const std::exception &e) {
+        set_error(std::string(fn) + ": " + e.what());
+        return IGR_ERR_INTERNAL;
+    } catch (...) {
+        set_error(std::string(fn) + ": unknown exception");
+        return IGR_ERR_INTERNAL;
+    }
+}
+
+inline int arg_error(const char *fn, const std::string &what) {
+    set_error(std::string(fn) + ": " + what);
+    return IGR_ERR_ARG;
+}
+
+inline int launch_status(const char *fn) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error(std::string(fn) + ": " + hipGetErrorString(e));
+        return IGR_ERR_HIP;
+    }
+    return IGR_OK;
+}
+
+inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+}  // namespace igr
+
+// ---------------------------------------------------------------- device helpers
+#ifdef __HIPCC__
+namespace igr {
+
+__device__ __forceinline__ float4 f4_fma(float w, float4 x, float4 a) {
+    a.x = fmaf(w, x.x, a.x);
+    a.y = fmaf(w, x.y, a.y);
+    a.z = fmaf(w, x.z, a.z);
+    a.w = fmaf(w, x.w, a.w);
+    return a;
+}
+
+__device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+__device__ __forceinline__ float4 f4_scale(float s, float4 a) {
+    return make_float4(s * a.x, s * a.y, s * a.z, s * a.w);
+}
+
+__device__ __forceinline__ float4 f4_div(float4 a, float s) {
+    return make_float4(a.x / s, a.y / s, a.z / s, a.w / s);
+}
+
+// Streamed-once loads (CSR structure, edge values): keep them out of the way
+// of the gathered feature table in L2 / Infinity Cache.
+template <class T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+    return __builtin_nontemporal_load(p);
+}
+
+// Lane shuffle within the wave (ds_bpermute).
+__device__ __forceinline__ int shfl_i(int v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ float shfl_xor_f(float v, int m) { return __shfl_xor(v, m, 64); }
+
+}  // namespace igr
+#endif

@@ -1,0 +1,333 @@
+// edge_ops.hip - per-edge kernels of the attention inductive layer and the
+// feature-matrix value updates (gfx950).
+//
+//   igr_sddmm_dot_f32         AttIGCN.masked_mm            model.py:4246-4255
+//   igr_segment_reduce_f32    gspmm copy_rhs max/sum       model.py:4270, 4273
+//   igr_att_softmax_f32(+bwd) edge softmax + head mean     model.py:4270-4275
+//   igr_edge_dropout_f32      NGCF.dropout_sp_mat          model.py:4016-4028
+//   igr_feat_values_f32       IGCN.update_feat_mat         model.py:4127-4130
+#include <cmath>
+
+#include "common.h"
+
+namespace igr {
+
+// ---------------------------------------------------------------- SDDMM
+// One wave per destination row.  A node row holds TOT = h*d floats; LPE =
+// TOT/4 lanes read one with a float4 each, so a wave covers EPW = 64/LPE
+// edges at a time.  The row's u slice stays in registers; each edge gathers
+// one v row (TOT*4 bytes) and reduces its d/4-lane head segments with xor
+// shuffles (wave-converged: every lane runs the same trip count).
+template <int TOT>
+__global__ __launch_bounds__(256) void sddmm_dot_kernel(
+    int64_t n_rows, int h, int d, const int64_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const int64_t *__restrict__ eid, const float *__restrict__ u,
+    int64_t ld_u, const float *__restrict__ v, int64_t ld_v, float *__restrict__ out) {
+    constexpr int LPE = TOT / 4;
+    constexpr int EPW = 64 / LPE;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n_rows) return;
+    const int lane = threadIdx.x & 63;
+    const int eg = lane / LPE;
+    const int sub = lane - eg * LPE;
+    const int hs = d / 4;  // lanes per head (power of two, checked by the host)
+    const float4 uq = *reinterpret_cast<const float4 *>(u + r * ld_u + sub * 4);
+    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
+    for (int64_t base = b; base < e; base += EPW) {
+        const int64_t p = base + eg;
+        const bool ok = p < e;
+        float4 vk = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) vk = *reinterpret_cast<const float4 *>(v + (int64_t)col[p] * ld_v + sub * 4);
+        float s = uq.x * vk.x + uq.y * vk.y + uq.z * vk.z + uq.w * vk.w;
+        for (int m = hs >> 1; m >= 1; m >>= 1) s += shfl_xor_f(s, m);
+        if (ok && (sub % hs) == 0) {
+            const int64_t ed = eid ? eid[p] : p;
+            out[ed * h + sub / hs] = s;
+        }
+    }
+}
+
+// Any shape: one thread per (edge, head).
+__global__ void sddmm_dot_generic(int64_t n_rows, int h, int d, const int64_t *__restrict__ row_ptr,
+                                  const int32_t *__restrict__ col, const int64_t *__restrict__ eid,
+                                  const float *__restrict__ u, int64_t ld_u,
+                                  const float *__restrict__ v, int64_t ld_v, float *__restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n_rows) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
+    for (int64_t t = lane; t < (e - b) * h; t += 64) {
+        const int64_t p = b + t / h;
+        const int j = (int)(t % h);
+        const float *a = u + r * ld_u + (int64_t)j * d;
+        const float *c = v + (int64_t)col[p] * ld_v + (int64_t)j * d;
+        float s = 0.f;
+        for (int k = 0; k < d; ++k) s = fmaf(a[k], c[k], s);
+        out[(eid ? eid[p] : p) * h + j] = s;
+    }
+}
+
+// ---------------------------------------------------------------- wave reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_f(v, m);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, shfl_xor_f(v, m));
+    return v;
+}
+
+// ---------------------------------------------------------------- copy_rhs reduce
+__global__ __launch_bounds__(256) void segment_reduce_kernel(int64_t n_rows, int h,
+                                                             const int64_t *__restrict__ row_ptr,
+                                                             const int64_t *__restrict__ eid,
+                                                             const float *__restrict__ x, int reduce,
+                                                             float *__restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n_rows) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
+    for (int j = 0; j < h; ++j) {
+        float a = reduce ? -INFINITY : 0.f;
+        for (int64_t p = b + lane; p < e; p += 64) {
+            const float t = x[(eid ? eid[p] : p) * h + j];
+            a = reduce ? fmaxf(a, t) : a + t;
+        }
+        a = reduce ? wave_max(a) : wave_sum(a);
+        if (lane == 0) out[r * h + j] = (b == e) ? 0.f : a;
+    }
+}
+
+// ---------------------------------------------------------------- attention edge softmax
+constexpr int kMaxHeads = 8;
+
+// z = (alpha - m) / sqrt_d / 10, computed as the two divisions the reference writes.
+__device__ __forceinline__ float att_exp(float a, float m, float sqrt_d) {
+    return expf((a - m) / sqrt_d / 10.f);
+}
+
+__global__ __launch_bounds__(256) void att_softmax_kernel(
+    int64_t n_rows, int h, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
+    const float *__restrict__ alpha, float sqrt_d, float *__restrict__ w,
+    float *__restrict__ row_max, float *__restrict__ row_sum) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n_rows) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
+    float m[kMaxHeads], s[kMaxHeads];
+#pragma unroll
+    for (int j = 0; j < kMaxHeads; ++j) {
+        m[j] = -INFINITY;
+        s[j] = 0.f;
+    }
+    for (int64_t p = b + lane; p < e; p += 64) {
+        const float *a = alpha + (eid ? eid[p] : p) * h;
+#pragma unroll
+        for (int j = 0; j < kMaxHeads; ++j)
+            if (j < h) m[j] = fmaxf(m[j], a[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxHeads; ++j)
+        if (j < h) m[j] = wave_max(m[j]);
+    for (int64_t p = b + lane; p < e; p += 64) {
+        const float *a = alpha + (eid ? eid[p] : p) * h;
+#pragma unroll
+        for (int j = 0; j < kMaxHeads; ++j)
+            if (j < h) s[j] += att_exp(a[j], m[j], sqrt_d);
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxHeads; ++j)
+        if (j < h) s[j] = wave_sum(s[j]);
+    if (lane == 0 && b < e) {
+        for (int j = 0; j < h; ++j) {
+            if (row_max) row_max[r * h + j] = m[j];
+            if (row_sum) row_sum[r * h + j] = s[j];
+        }
+    }
+    for (int64_t p = b + lane; p < e; p += 64) {
+        const int64_t ed = eid ? eid[p] : p;
+        const float *a = alpha + ed * h;
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < kMaxHeads; ++j)
+            if (j < h) acc += att_exp(a[j], m[j], sqrt_d) / s[j];
+        w[ed] = acc / (float)h;
+    }
+}
+
+// d alpha[e,j] = a_ej (g_e/h - S_j) / (sqrt_d * 10),  S_j = sum_e a_ej g_e / h,
+// a_ej = softmax weight of head j.  The path through the row max carries an
+// exactly-zero gradient (softmax is shift invariant) and is omitted.
+__global__ __launch_bounds__(256) void att_softmax_bwd_kernel(
+    int64_t n_rows, int h, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
+    const float *__restrict__ alpha, float sqrt_d, const float *__restrict__ row_max,
+    const float *__restrict__ row_sum, const float *__restrict__ dw, float *__restrict__ dalpha) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n_rows) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
+    if (b == e) return;
+    float m[kMaxHeads], s[kMaxHeads], S[kMaxHeads];
+#pragma unroll
+    for (int j = 0; j < kMaxHeads; ++j) {
+        m[j] = (j < h) ? row_max[r * h + j] : 0.f;
+        s[j] = (j < h) ? row_sum[r * h + j] : 1.f;
+        S[j] = 0.f;
+    }
+    const float inv_h = 1.f / (float)h;
+    for (int64_t p = b + lane; p < e; p += 64) {
+        const int64_t ed = eid ? eid[p] : p;
+        const float g = dw[ed] * inv_h;
+#pragma unroll
+        for (int j = 0; j < kMaxHeads; ++j)
+            if (j < h) S[j] += att_exp(alpha[ed * h + j], m[j], sqrt_d) / s[j] * g;
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxHeads; ++j)
+        if (j < h) S[j] = wave_sum(S[j]);
+    const float c = sqrt_d * 10.f;
+    for (int64_t p = b + lane; p < e; p += 64) {
+        const int64_t ed = eid ? eid[p] : p;
+        const float g = dw[ed] * inv_h;
+#pragma unroll
+        for (int j = 0; j < kMaxHeads; ++j)
+            if (j < h) {
+                const float a = att_exp(alpha[ed * h + j], m[j], sqrt_d) / s[j];
+                dalpha[ed * h + j] = a * (g - S[j]) / c;
+            }
+    }
+}
+
+// ---------------------------------------------------------------- value kernels
+__global__ void edge_dropout_kernel(int64_t n, const float *__restrict__ val,
+                                    const float *__restrict__ rand, float keep,
+                                    float *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        // random_tensor = (1 - p) + U; mask = floor(random_tensor) (model.py:4019-4021)
+        const bool k = floorf(keep + rand[i]) != 0.f;
+        out[i] = k ? val[i] / keep : 0.f;
+    }
+}
+
+__global__ void feat_values_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr,
+                                   const float *__restrict__ row_sum, float ex,
+                                   float *__restrict__ out) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_rows;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        const float x = row_sum[r];
+        // torch.pow(t, -0.5) lowers to rsqrt (1 / sqrt); other exponents to pow
+        const float v = (ex == -0.5f) ? 1.f / sqrtf(x) : powf(x, ex);
+        for (int64_t p = row_ptr[r]; p < row_ptr[r + 1]; ++p) out[p] = v;
+    }
+}
+
+static unsigned grid_for(int64_t n, int block) {
+    int64_t g = (n + block - 1) / block;
+    if (g > 8192) g = 8192;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+
+static bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
+}  // namespace igr
+
+using namespace igr;
+
+extern "C" int igr_sddmm_dot_f32(const igr_csr *g, int32_t h, int32_t d, const float *u,
+                                 int64_t ld_u, const float *v, int64_t ld_v, float *out,
+                                 void *stream) {
+    return guarded("igr_sddmm_dot_f32", [&]() -> int {
+        const char *fn = "igr_sddmm_dot_f32";
+        if (!g || h <= 0 || d <= 0) return arg_error(fn, "bad graph / h / d");
+        if (ld_u < (int64_t)h * d || ld_v < (int64_t)h * d) return arg_error(fn, "leading dimension < h*d");
+        if (g->n_rows == 0 || g->nnz == 0) return IGR_OK;
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        const unsigned blocks = (unsigned)((g->n_rows + 3) / 4);
+        const int tot = h * d;
+        const bool vec = (d % 4 == 0) && pow2(d / 4) && ld_u % 4 == 0 && ld_v % 4 == 0 &&
+                         aligned16(u) && aligned16(v);
+#define IGR_SDDMM(T)                                                                              \
+    hipLaunchKernelGGL((sddmm_dot_kernel<T>), dim3(blocks), dim3(256), 0, st, g->n_rows, h, d,   \
+                       g->row_ptr, g->col_idx, g->edge_id, u, ld_u, v, ld_v, out)
+        if (vec && tot == 64) IGR_SDDMM(64);
+        else if (vec && tot == 128) IGR_SDDMM(128);
+        else if (vec && tot == 256) IGR_SDDMM(256);
+        else if (vec && tot == 32) IGR_SDDMM(32);
+        else
+            hipLaunchKernelGGL(sddmm_dot_generic, dim3(blocks), dim3(256), 0, st, g->n_rows, h, d,
+                               g->row_ptr, g->col_idx, g->edge_id, u, ld_u, v, ld_v, out);
+#undef IGR_SDDMM
+        return launch_status(fn);
+    });
+}
+
+extern "C" int igr_segment_reduce_f32(const igr_csr *g, int32_t h, const float *x, int32_t reduce,
+                                      float *out, void *stream) {
+    return guarded("igr_segment_reduce_f32", [&]() -> int {
+        const char *fn = "igr_segment_reduce_f32";
+        if (!g || h <= 0) return arg_error(fn, "bad graph / h");
+        if (reduce != 0 && reduce != 1) return arg_error(fn, "reduce must be 0 (sum) or 1 (max)");
+        if (g->n_rows == 0) return IGR_OK;
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        hipLaunchKernelGGL(segment_reduce_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256),
+                           0, st, g->n_rows, h, g->row_ptr, g->edge_id, x, reduce, out);
+        return launch_status(fn);
+    });
+}
+
+extern "C" int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alpha, float sqrt_d,
+                                   float *w, float *row_max, float *row_sum, void *stream) {
+    return guarded("igr_att_softmax_f32", [&]() -> int {
+        const char *fn = "igr_att_softmax_f32";
+        if (!g || h <= 0 || h > kMaxHeads) return arg_error(fn, "h must be in [1, 8]");
+        if (g->n_rows == 0) return IGR_OK;
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        hipLaunchKernelGGL(att_softmax_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0,
+                           st, g->n_rows, h, g->row_ptr, g->edge_id, alpha, sqrt_d, w, row_max,
+                           row_sum);
+        return launch_status(fn);
+    });
+}
+
+extern "C" int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float *alpha,
+                                       float sqrt_d, const float *row_max, const float *row_sum,
+                                       const float *dw, float *dalpha, void *stream) {
+    return guarded("igr_att_softmax_bwd_f32", [&]() -> int {
+        const char *fn = "igr_att_softmax_bwd_f32";
+        if (!g || h <= 0 || h > kMaxHeads) return arg_error(fn, "h must be in [1, 8]");
+        if (!row_max || !row_sum) return arg_error(fn, "row_max / row_sum required");
+        if (g->n_rows == 0) return IGR_OK;
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        hipLaunchKernelGGL(att_softmax_bwd_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256),
+                           0, st, g->n_rows, h, g->row_ptr, g->edge_id, alpha, sqrt_d, row_max,
+                           row_sum, dw, dalpha);
+        return launch_status(fn);
+    });
+}
+
+extern "C" int igr_edge_dropout_f32(int64_t n, const float *val, const float *rand, float p,
+                                    float *out, void *stream) {
+    return guarded("igr_edge_dropout_f32", [&]() -> int {
+        if (!(p >= 0.f && p < 1.f)) return arg_error("igr_edge_dropout_f32", "p must be in [0, 1)");
+        if (n <= 0) return IGR_OK;
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        const float keep = (float)(1.0 - (double)p);
+        hipLaunchKernelGGL(edge_dropout_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, n, val,
+                           rand, keep, out);
+        return launch_status("igr_edge_dropout_f32");
+    });
+}
+
+extern "C" int igr_feat_values_f32(int64_t n_rows, const int64_t *row_ptr, const float *row_sum,
+                                   float exponent, float *out, void *stream) {
+    return guarded("igr_feat_values_f32", [&]() -> int {
+        if (n_rows <= 0) return IGR_OK;
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        hipLaunchKernelGGL(feat_values_kernel, dim3(grid_for(n_rows, 256)), dim3(256), 0, st,
+                           n_rows, row_ptr, row_sum, exponent, out);
+        return launch_status("igr_feat_values_f32");
+    });
+}

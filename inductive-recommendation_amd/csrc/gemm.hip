@@ -1,0 +1,115 @@
+// gemm.hip - fp32 GEMM on gfx950 matrix cores (v_mfma_f32_16x16x4_f32).
+//
+// The dense projections on the GCN path: NGCF gc/bi layers Linear(d, d)
+// (model.py:3998-4004, 4039) and AttIGCN weight_q / weight_k Linear(d, 4d)
+// (model.py:4242-4243, 4259, 4264), forward and backward.  Shapes are tall and
+// skinny (M = node count, N, K = d..4d), so one 64x64 output tile per
+// workgroup, K staged through LDS 16 at a time.  f32-input MFMA is an exact
+// k-ordered fmaf chain (no xf32 on gfx950), i.e. fp32 semantics.
+#include "common.h"
+
+namespace igr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 64, BN = 64, BK = 16;
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_f32_mfma(int64_t M, int64_t N, int64_t K,
+                                                     const float *__restrict__ A, int64_t lda,
+                                                     const float *__restrict__ B, int64_t ldb,
+                                                     const float *__restrict__ bias,
+                                                     float *__restrict__ C, int64_t ldc) {
+    // LDS images [k][m] and [k][n], padded by one float to break bank strides.
+    __shared__ float As[BK][BM + 1];
+    __shared__ float Bs[BK][BN + 1];
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves, 32x32 each
+    const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int64_t k0 = 0; k0 < K; k0 += BK) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int idx = t + i * 256;
+            int mm, kk;
+            if (TA) { kk = idx / BM; mm = idx % BM; }   // a[k*lda + m]: m contiguous
+            else { mm = idx / BK; kk = idx % BK; }      // a[m*lda + k]: k contiguous
+            const int64_t gm = m0 + mm, gk = k0 + kk;
+            float v = 0.f;
+            if (gm < M && gk < K) v = TA ? A[gk * lda + gm] : A[gm * lda + gk];
+            As[kk][mm] = v;
+            int nn;
+            if (TB) { kk = idx / BN; nn = idx % BN; }   // b[k*ldb + n]
+            else { nn = idx / BK; kk = idx % BK; }      // b[n*ldb + k] (Linear weight)
+            const int64_t gn = n0 + nn, gk2 = k0 + kk;
+            float w = 0.f;
+            if (gn < N && gk2 < K) w = TB ? B[gk2 * ldb + gn] : B[gn * ldb + gk2];
+            Bs[kk][nn] = w;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < BK; ks += 4) {
+            const int kr = ks + (lane >> 4);
+            float a[2], b[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) a[i] = As[kr][wm * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b[j] = Bs[kr][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // C/D map of 16x16x4: col = lane & 15, row = (lane >> 4) * 4 + reg
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int64_t gn = n0 + wn * 32 + j * 16 + (lane & 15);
+            if (gn >= N) continue;
+            const float bv = bias ? bias[gn] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t gm = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+                if (gm < M) C[gm * ldc + gn] = acc[i][j][r] + bv;
+            }
+        }
+}
+
+}  // namespace igr
+
+using namespace igr;
+
+extern "C" int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int64_t lda,
+                            int32_t trans_a, const float *b, int64_t ldb, int32_t trans_b,
+                            const float *bias, float *c, int64_t ldc, void *stream) {
+    return guarded("igr_gemm_f32", [&]() -> int {
+        const char *fn = "igr_gemm_f32";
+        if (m < 0 || n < 0 || k < 0) return arg_error(fn, "negative size");
+        if (ldc < n) return arg_error(fn, "ldc < n");
+        if ((trans_a ? lda < m : lda < k) || (trans_b ? ldb < n : ldb < k))
+            return arg_error(fn, "leading dimension too small");
+        if (m == 0 || n == 0) return IGR_OK;
+        if ((n + BN - 1) / BN > 65535) return arg_error(fn, "n too large");
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        dim3 grid((unsigned)((m + BM - 1) / BM), (unsigned)((n + BN - 1) / BN));
+        if (trans_a && trans_b)
+            hipLaunchKernelGGL((gemm_f32_mfma<true, true>), grid, dim3(256), 0, st, m, n, k, a, lda, b, ldb, bias, c, ldc);
+        else if (trans_a)
+            hipLaunchKernelGGL((gemm_f32_mfma<true, false>), grid, dim3(256), 0, st, m, n, k, a, lda, b, ldb, bias, c, ldc);
+        else if (trans_b)
+            hipLaunchKernelGGL((gemm_f32_mfma<false, true>), grid, dim3(256), 0, st, m, n, k, a, lda, b, ldb, bias, c, ldc);
+        else
+            hipLaunchKernelGGL((gemm_f32_mfma<false, false>), grid, dim3(256), 0, st, m, n, k, a, lda, b, ldb, bias, c, ldc);
+        return launch_status(fn);
+    });
+}

@@ -1,0 +1,355 @@
+// spmm.hip - CSR SpMM (DGL gspmm 'mul'/'sum') for gfx950.
+//
+// Replaces dgl.ops.gspmm(g, 'mul', 'sum', lhs, rhs) at model.py:106, 4184,
+// 4196, 4037 and its reverse-graph backward:
+//     y[r] = sum_{p in row r} rhs[eid(p)] * x[col[p]]          (fp32)
+//
+// Design:
+//  * One feature row of x is D fp32 = D/4 float4; LPR = D/4 lanes cover it
+//    with one 16-B load each, so a wave64 holds G = 64/LPR rows.
+//  * Row tier: each LPR-lane group owns one output row.  Rows are visited in
+//    degree-descending order (igr_plan_fill), so the G rows of a wave have
+//    ~equal degree (no intra-wave imbalance) and the heaviest rows start
+//    first (no tail).  A group loads LPR (col, val) pairs with one coalesced
+//    load, broadcasts them with ds_bpermute, and keeps 8 row gathers in
+//    flight; the next block of (col, val) is prefetched under the gathers.
+//  * Chunk tier: rows longer than split_threshold are cut into fixed-size
+//    chunks; one wave per chunk, each group taking its own LPR-edge slice of
+//    every 64-edge block, then a cross-group xor reduction, and a partial row written to a workspace.
+//    A second kernel sums each row's partials in chunk order.  No atomics:
+//    results are bitwise reproducible run to run.
+//  * Both tiers run in ONE launch (chunk blocks first, heaviest work first).
+//  * The row epilogue fuses the LightGCN/IGCN layer mean and the backward's
+//    "+ g/(L+1)" (igr_epilogue).
+//  * CSR structure and edge values are streamed with non-temporal loads so
+//    the gathered x table keeps the L2 / Infinity Cache.
+#include <algorithm>
+
+#include "common.h"
+
+namespace igr {
+
+struct Epi {
+    float *y;
+    int64_t ldy;
+    float alpha, beta;
+    const float *add;
+    int64_t ld_add;
+    float *acc;
+    int64_t ld_acc;
+    int acc_mode;
+    float acc_div;
+    int skip_y;
+};
+
+__device__ __forceinline__ void store_row4(const Epi &e, int64_t r, int f, float4 s) {
+    float4 y = s;
+    if (e.alpha != 1.f) y = f4_scale(e.alpha, y);
+    if (e.add) {
+        float4 a = *reinterpret_cast<const float4 *>(e.add + r * e.ld_add + f);
+        y = f4_fma(e.beta, a, y);
+    }
+    if (!e.skip_y) *reinterpret_cast<float4 *>(e.y + r * e.ldy + f) = y;
+    if (e.acc_mode) {
+        float4 *ap = reinterpret_cast<float4 *>(e.acc + r * e.ld_acc + f);
+        float4 a = (e.acc_mode == 2) ? f4_add(*ap, y) : y;
+        if (e.acc_div != 1.f) a = f4_div(a, e.acc_div);
+        *ap = a;
+    }
+}
+
+__device__ __forceinline__ void store_row1(const Epi &e, int64_t r, int f, float s) {
+    float y = e.alpha * s;
+    if (e.add) y = fmaf(e.beta, e.add[r * e.ld_add + f], y);
+    if (!e.skip_y) e.y[r * e.ldy + f] = y;
+    if (e.acc_mode) {
+        float a = (e.acc_mode == 2) ? e.acc[r * e.ld_acc + f] + y : y;
+        e.acc[r * e.ld_acc + f] = a / e.acc_div;
+    }
+}
+
+template <bool VAL, bool EID>
+__device__ __forceinline__ float edge_weight(const float *__restrict__ val,
+                                             const int64_t *__restrict__ eid, int64_t p) {
+    if constexpr (!VAL) {
+        return 1.f;
+    } else if constexpr (EID) {
+        return val[ld_stream(eid + p)];
+    } else {
+        return ld_stream(val + p);
+    }
+}
+
+constexpr int kUnroll = 8;
+
+// Accumulate the first n edges of a block whose (col, val) pairs live in lanes
+// gbase .. gbase+n-1 of the caller's own lane group (shuffles never leave the
+// group, so divergence between groups is harmless).  All loads of a step of
+// kUnroll are issued before their FMAs.
+__device__ __forceinline__ float4 gather_block(float4 acc, int cl, float vl, int gbase, int n,
+                                               const float *__restrict__ xs, int64_t ldx) {
+    int k = 0;
+    for (; k + kUnroll <= n; k += kUnroll) {
+        float4 xv[kUnroll];
+        float wv[kUnroll];
+#pragma unroll
+        for (int j = 0; j < kUnroll; ++j) {
+            const int c = shfl_i(cl, gbase + (k + j));
+            wv[j] = shfl_f(vl, gbase + (k + j));
+            xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
+        }
+#pragma unroll
+        for (int j = 0; j < kUnroll; ++j) acc = f4_fma(wv[j], xv[j], acc);
+    }
+    if (k < n) {
+        // predicated remainder: out-of-range slots re-read the last valid row
+        // (a cache hit) and are masked out of the sum.
+        float4 xv[kUnroll];
+        float wv[kUnroll];
+        const int last = n - 1;
+#pragma unroll
+        for (int j = 0; j < kUnroll; ++j) {
+            const int kk = min(k + j, last);
+            const int c = shfl_i(cl, gbase + kk);
+            wv[j] = shfl_f(vl, gbase + kk);
+            xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
+        }
+#pragma unroll
+        for (int j = 0; j < kUnroll; ++j)
+            if (k + j < n) acc = f4_fma(wv[j], xv[j], acc);
+    }
+    return acc;
+}
+
+template <int D, bool VAL, bool EID>
+__global__ __launch_bounds__(256) void spmm_main(
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+    const int64_t *__restrict__ eid, const float *__restrict__ val, const float *__restrict__ x,
+    int64_t ldx, const int32_t *__restrict__ order, int64_t n_order,
+    const int32_t *__restrict__ chunk_row, const int64_t *__restrict__ chunk_beg, int64_t n_chunks,
+    int64_t chunk_edges, float *__restrict__ ws, int64_t chunk_blocks, Epi epi) {
+    constexpr int LPR = D / 4;   // lanes per feature row
+    constexpr int G = 64 / LPR;  // groups per wave
+    const int lane = threadIdx.x & 63;
+    const int grp = lane / LPR;
+    const int sub = lane - grp * LPR;
+    const int wib = threadIdx.x >> 6;
+    const float *xs = x + sub * 4;
+
+    if ((int64_t)blockIdx.x < chunk_blocks) {
+        // ---------------- chunk tier: one wave per chunk of a long row
+        const int64_t c = (int64_t)blockIdx.x * 4 + wib;
+        if (c >= n_chunks) return;
+        const int r = chunk_row[c];
+        const int64_t b = chunk_beg[c];
+        const int64_t e = min(b + chunk_edges, row_ptr[r + 1]);
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        int64_t base = b;
+        int n = (int)min((int64_t)64, e - base);
+        int cl = 0;
+        float vl = 0.f;
+        if (lane < n) {
+            cl = ld_stream(col + base + lane);
+            vl = edge_weight<VAL, EID>(val, eid, base + lane);
+        }
+        while (n > 0) {
+            const int64_t nb = base + 64;
+            const int nn = (int)min((int64_t)64, e - nb);
+            int cl2 = 0;
+            float vl2 = 0.f;
+            if (lane < nn) {
+                cl2 = ld_stream(col + nb + lane);
+                vl2 = edge_weight<VAL, EID>(val, eid, nb + lane);
+            }
+            // group grp takes edges [grp*LPR, grp*LPR + LPR) of this 64-edge block,
+            // i.e. exactly the (col, val) pairs its own lanes loaded
+            const int m = min(max(n - grp * LPR, 0), LPR);
+            acc = gather_block(acc, cl, vl, grp * LPR, m, xs, ldx);
+            base = nb;
+            n = nn;
+            cl = cl2;
+            vl = vl2;
+        }
+#pragma unroll
+        for (int s = LPR; s < 64; s <<= 1) {
+            acc.x += shfl_xor_f(acc.x, s);
+            acc.y += shfl_xor_f(acc.y, s);
+            acc.z += shfl_xor_f(acc.z, s);
+            acc.w += shfl_xor_f(acc.w, s);
+        }
+        if (grp == 0) *reinterpret_cast<float4 *>(ws + c * D + sub * 4) = acc;
+        return;
+    }
+
+    // ---------------- row tier: one LPR-lane group per row
+    const int64_t w = ((int64_t)blockIdx.x - chunk_blocks) * 4 + wib;
+    const int64_t i = w * G + grp;
+    if (i >= n_order) return;
+    const int r = order[i];
+    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
+    const int gbase = grp * LPR;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t base = b;
+    int n = (int)min((int64_t)LPR, e - base);
+    int cl = 0;
+    float vl = 0.f;
+    if (sub < n) {
+        cl = ld_stream(col + base + sub);
+        vl = edge_weight<VAL, EID>(val, eid, base + sub);
+    }
+    while (n > 0) {
+        const int64_t nb = base + LPR;
+        const int nn = (int)min((int64_t)LPR, e - nb);
+        int cl2 = 0;
+        float vl2 = 0.f;
+        if (sub < nn) {
+            cl2 = ld_stream(col + nb + sub);
+            vl2 = edge_weight<VAL, EID>(val, eid, nb + sub);
+        }
+        acc = gather_block(acc, cl, vl, gbase, n, xs, ldx);
+        base = nb;
+        n = nn;
+        cl = cl2;
+        vl = vl2;
+    }
+    store_row4(epi, r, sub * 4, acc);
+}
+
+// Sum each split row's chunk partials in chunk order, then the epilogue.
+template <int D>
+__global__ __launch_bounds__(256) void spmm_combine(const int32_t *__restrict__ split_row,
+                                                    const int64_t *__restrict__ split_ptr,
+                                                    int64_t n_split, const float *__restrict__ ws,
+                                                    Epi epi) {
+    constexpr int LPR = D / 4;
+    constexpr int G = 64 / LPR;
+    const int lane = threadIdx.x & 63;
+    const int grp = lane / LPR;
+    const int sub = lane - grp * LPR;
+    const int64_t i = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G + grp;
+    if (i >= n_split) return;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t c = split_ptr[i]; c < split_ptr[i + 1]; ++c)
+        acc = f4_add(acc, *reinterpret_cast<const float4 *>(ws + c * D + sub * 4));
+    store_row4(epi, split_row[i], sub * 4, acc);
+}
+
+// Any d / alignment: one wave per row, lanes over features.
+template <bool VAL, bool EID>
+__global__ __launch_bounds__(256) void spmm_generic(int64_t n_rows, int d,
+                                                    const int64_t *__restrict__ row_ptr,
+                                                    const int32_t *__restrict__ col,
+                                                    const int64_t *__restrict__ eid,
+                                                    const float *__restrict__ val,
+                                                    const float *__restrict__ x, int64_t ldx,
+                                                    Epi epi) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= n_rows) return;
+    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
+    for (int f = lane; f < d; f += 64) {
+        float s = 0.f;
+        for (int64_t p = b; p < e; ++p) s = fmaf(edge_weight<VAL, EID>(val, eid, p), x[(int64_t)col[p] * ldx + f], s);
+        store_row1(epi, r, f, s);
+    }
+}
+
+template <int D, bool VAL, bool EID>
+static void launch_fast(const igr_csr *g, const float *x, int64_t ldx, const float *rhs,
+                        const Epi &epi, float *ws, hipStream_t st) {
+    constexpr int G = 64 / (D / 4);
+    const int64_t chunk_blocks = (g->n_chunks + 3) / 4;
+    const int64_t row_blocks = (g->n_order + 4 * G - 1) / (4 * G);
+    const int64_t blocks = chunk_blocks + row_blocks;
+    if (blocks > 0)
+        hipLaunchKernelGGL((spmm_main<D, VAL, EID>), dim3((unsigned)blocks), dim3(256), 0, st,
+                           g->row_ptr, g->col_idx, g->edge_id, rhs, x, ldx, g->order, g->n_order,
+                           g->chunk_row, g->chunk_beg, g->n_chunks, g->chunk_edges, ws,
+                           chunk_blocks, epi);
+    if (g->n_split > 0) {
+        const int64_t cb = (g->n_split + 4 * G - 1) / (4 * G);
+        hipLaunchKernelGGL((spmm_combine<D>), dim3((unsigned)cb), dim3(256), 0, st, g->split_row,
+                           g->split_ptr, g->n_split, ws, epi);
+    }
+}
+
+template <int D>
+static void dispatch_fast(const igr_csr *g, const float *x, int64_t ldx, const float *rhs,
+                          const Epi &epi, float *ws, hipStream_t st) {
+    const bool val = rhs != nullptr, eid = g->edge_id != nullptr;
+    if (val && eid) launch_fast<D, true, true>(g, x, ldx, rhs, epi, ws, st);
+    else if (val) launch_fast<D, true, false>(g, x, ldx, rhs, epi, ws, st);
+    else launch_fast<D, false, false>(g, x, ldx, rhs, epi, ws, st);
+}
+
+}  // namespace igr
+
+using namespace igr;
+
+extern "C" int igr_spmm_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx,
+                            const float *rhs, float *y, int64_t ldy, const igr_epilogue *epi_in,
+                            float *workspace, void *stream) {
+    return guarded("igr_spmm_f32", [&]() -> int {
+        const char *fn = "igr_spmm_f32";
+        if (!g) return arg_error(fn, "graph is NULL");
+        if (d <= 0) return arg_error(fn, "d must be positive");
+        if (g->n_rows < 0 || g->n_cols < 0 || g->nnz < 0) return arg_error(fn, "negative sizes");
+        if (g->n_rows == 0) return IGR_OK;
+        if (!g->row_ptr || (g->nnz > 0 && !g->col_idx)) return arg_error(fn, "missing CSR arrays");
+        if (g->nnz > 0 && !x) return arg_error(fn, "x is NULL");
+        if (ldx < d || ldy < d) return arg_error(fn, "leading dimension smaller than d");
+        if (g->n_order + g->n_split != g->n_rows)
+            return arg_error(fn, "schedule does not cover every row (n_order + n_split != n_rows)");
+        if (g->n_chunks > 0 && !workspace) return arg_error(fn, "workspace required for split rows");
+        Epi e{};
+        e.y = y;
+        e.ldy = ldy;
+        e.alpha = 1.f;
+        e.beta = 0.f;
+        e.acc_div = 1.f;
+        if (epi_in) {
+            e.alpha = epi_in->alpha;
+            e.beta = epi_in->beta;
+            e.add = epi_in->add;
+            e.ld_add = epi_in->ld_add;
+            e.acc = epi_in->acc;
+            e.ld_acc = epi_in->ld_acc;
+            e.acc_mode = epi_in->acc_mode;
+            e.acc_div = epi_in->acc_div;
+            e.skip_y = epi_in->skip_y;
+            if (e.acc_mode < 0 || e.acc_mode > 2) return arg_error(fn, "acc_mode must be 0, 1 or 2");
+            if (e.acc_mode && (!e.acc || e.ld_acc < d)) return arg_error(fn, "bad acc");
+            if (e.add && e.ld_add < d) return arg_error(fn, "bad ld_add");
+            if (e.acc_div == 0.f) return arg_error(fn, "acc_div is 0");
+        }
+        if (!e.skip_y && !y) return arg_error(fn, "y is NULL");
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+
+        bool fast = (d == 32 || d == 64 || d == 128 || d == 256) && (ldx % 4 == 0) &&
+                    (ldy % 4 == 0) && aligned16(x) && aligned16(y) && aligned16(workspace);
+        if (e.add) fast = fast && aligned16(e.add) && e.ld_add % 4 == 0;
+        if (e.acc_mode) fast = fast && aligned16(e.acc) && e.ld_acc % 4 == 0;
+        if (fast) {
+            if (!g->order && g->n_order > 0) return arg_error(fn, "missing schedule");
+            switch (d) {
+                case 32: dispatch_fast<32>(g, x, ldx, rhs, e, workspace, st); break;
+                case 64: dispatch_fast<64>(g, x, ldx, rhs, e, workspace, st); break;
+                case 128: dispatch_fast<128>(g, x, ldx, rhs, e, workspace, st); break;
+                default: dispatch_fast<256>(g, x, ldx, rhs, e, workspace, st); break;
+            }
+        } else {
+            const unsigned blocks = (unsigned)((g->n_rows + 3) / 4);
+            const bool val = rhs != nullptr, eid = g->edge_id != nullptr;
+            if (val && eid)
+                hipLaunchKernelGGL((spmm_generic<true, true>), dim3(blocks), dim3(256), 0, st, g->n_rows, d,
+                                   g->row_ptr, g->col_idx, g->edge_id, rhs, x, ldx, e);
+            else if (val)
+                hipLaunchKernelGGL((spmm_generic<true, false>), dim3(blocks), dim3(256), 0, st, g->n_rows, d,
+                                   g->row_ptr, g->col_idx, g->edge_id, rhs, x, ldx, e);
+            else
+                hipLaunchKernelGGL((spmm_generic<false, false>), dim3(blocks), dim3(256), 0, st, g->n_rows, d,
+                                   g->row_ptr, g->col_idx, g->edge_id, rhs, x, ldx, e);
+        }
+        return launch_status(fn);
+    });
+}

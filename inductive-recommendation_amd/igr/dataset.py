@@ -1,0 +1,219 @@
+"""igr.dataset - the reference's dataset surface (dataset.py) for the path.
+
+ProcessedDataset reads the same train/val/test.txt format
+(dataset.py:140-164); BasicDataset.__getitem__ is the reference's BPR
+sampler (dataset.py:119-131).  BPRBatchSampler draws whole batches with the
+same distribution in vectorised numpy (the reference runs the per-sample
+Python sampler in 6 DataLoader workers, trainer.py:522-526).
+SyntheticDataset builds the benchmark's random bipartite graphs.
+"""
+import os
+import random
+import sys
+
+import numpy as np
+
+
+def get_dataset(config):
+    """dataset.py:10-14."""
+    config = config.copy()
+    dataset = getattr(sys.modules[__name__], config['name'])
+    return dataset(config)
+
+
+class BasicDataset:
+    """dataset.py:47-137 (attributes and sampler)."""
+
+    def __init__(self, dataset_config):
+        self.config = dataset_config
+        self.name = dataset_config['name']
+        self.device = dataset_config.get('device', 'cpu')
+        self.negative_sample_ratio = dataset_config.get('neg_ratio', 1)
+        self.n_users = 0
+        self.n_items = 0
+        self.train_data = None
+        self.val_data = None
+        self.test_data = None
+        self.train_array = None
+        self._pairs = None
+
+    @property
+    def train_pairs(self):
+        """train_array as int64 [E, 2] (cached)."""
+        if self._pairs is None:
+            self._pairs = np.asarray(self.train_array, dtype=np.int64).reshape(-1, 2)
+        return self._pairs
+
+    def __len__(self):
+        return len(self.train_array)
+
+    def __getitem__(self, index):
+        """dataset.py:119-131 verbatim semantics: uniform user with training
+        items, uniform positive, rejection-sampled negative."""
+        user = random.randint(0, self.n_users - 1)
+        while not self.train_data[user]:
+            user = random.randint(0, self.n_users - 1)
+        pos_item = np.random.choice(self.train_data[user])
+        data = [[user, pos_item] for _ in range(self.negative_sample_ratio)]
+        for idx in range(self.negative_sample_ratio):
+            neg_item = random.randint(0, self.n_items - 1)
+            while neg_item in self.train_data[user]:
+                neg_item = random.randint(0, self.n_items - 1)
+            data[idx].append(neg_item)
+        return np.array(data, dtype=np.int64)
+
+    def output_dataset(self, path):
+        """dataset.py:133-137."""
+        os.makedirs(path, exist_ok=True)
+        for name, data in [('train.txt', self.train_data), ('val.txt', self.val_data), ('test.txt', self.test_data)]:
+            with open(os.path.join(path, name), 'w') as f:
+                for user in range(len(data)):
+                    f.write(' '.join([str(user)] + [str(i) for i in data[user]]) + '\n')
+
+
+def read_split(file_path):
+    """dataset.py:156-164: one line per user, 'user item item ...'."""
+    data, n_items = [], 0
+    with open(file_path) as f:
+        lines = f.read().strip().split('\n')
+    for line in lines:
+        items = [int(x) for x in line.split(' ')[1:]]
+        if items:
+            n_items = max(n_items, max(items) + 1)
+        data.append(items)
+    return data, n_items
+
+
+class ProcessedDataset(BasicDataset):
+    """dataset.py:140-164."""
+
+    def __init__(self, dataset_config):
+        super().__init__(dataset_config)
+        path = dataset_config['path']
+        self.train_data, a = read_split(os.path.join(path, 'train.txt'))
+        self.val_data, b = read_split(os.path.join(path, 'val.txt'))
+        self.test_data, c = read_split(os.path.join(path, 'test.txt'))
+        self.n_items = max(a, b, c)
+        assert len(self.train_data) == len(self.val_data) == len(self.test_data)
+        self.n_users = len(self.train_data)
+        self.train_array = [[u, i] for u in range(self.n_users) for i in self.train_data[u]]
+
+
+class AuxiliaryDataset(BasicDataset):
+    """dataset.py:258-273: training data restricted to / renumbered by the
+    template-feature maps of an inductive model."""
+
+    def __init__(self, dataset, user_map, item_map):
+        self.name = 'AuxiliaryDataset'
+        self.n_users = len(user_map)
+        self.n_items = len(item_map)
+        self.device = dataset.device
+        self.negative_sample_ratio = 1
+        self.length = len(dataset)
+        self._pairs = None
+        self.train_data = [[] for _ in range(self.n_users)]
+        for o_user in range(dataset.n_users):
+            if o_user in user_map:
+                for o_item in dataset.train_data[o_user]:
+                    if o_item in item_map:
+                        self.train_data[user_map[o_user]].append(item_map[o_item])
+        self.train_array = [[u, i] for u in range(self.n_users) for i in self.train_data[u]]
+
+    def __len__(self):
+        return self.length
+
+
+class SyntheticDataset(BasicDataset):
+    """Random bipartite interactions: users ~ U[0, n_users),
+    items ~ U[0, n_items) or Zipf(s) ; duplicates kept in train_array and
+    summed by the graph build exactly as utils.generate_daj_mat does.
+    val/test hold `n_eval` random items per user (synthetic; metrics are not
+    meaningful, only shapes)."""
+
+    def __init__(self, dataset_config):
+        super().__init__(dataset_config)
+        self.n_users = int(dataset_config['n_users'])
+        self.n_items = int(dataset_config['n_items'])
+        n_edges = int(dataset_config['n_edges'])
+        seed = int(dataset_config.get('seed', 0))
+        self._pairs = synthetic_pairs(self.n_users, self.n_items, n_edges, seed,
+                                      dataset_config.get('item_dist', 'uniform'), dataset_config.get('zipf_s', 1.1))
+        self.train_array = self._pairs
+        self._train_data = None
+        self.val_data = self.test_data = None
+
+    @property
+    def train_data(self):
+        if self._train_data is None and self._pairs is not None:
+            order = np.argsort(self._pairs[:, 0], kind='stable')
+            items = self._pairs[order, 1]
+            ptr = np.searchsorted(self._pairs[order, 0], np.arange(self.n_users + 1))
+            self._train_data = [items[ptr[u]:ptr[u + 1]].tolist() for u in range(self.n_users)]
+        return self._train_data
+
+    @train_data.setter
+    def train_data(self, v):
+        self._train_data = v
+
+
+def synthetic_pairs(n_users, n_items, n_edges, seed=0, item_dist='uniform', zipf_s=1.1):
+    """int64 [n_edges, 2] (user, item) draws with torch's CPU generator."""
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    u = torch.randint(0, n_users, (n_edges,), generator=g, dtype=torch.int64)
+    if item_dist == 'uniform':
+        i = torch.randint(0, n_items, (n_edges,), generator=g, dtype=torch.int64)
+    elif item_dist == 'zipf':
+        w = 1.0 / torch.arange(1, n_items + 1, dtype=torch.float64) ** zipf_s
+        i = torch.multinomial(w / w.sum(), n_edges, replacement=True, generator=g)
+    else:
+        raise ValueError(item_dist)
+    return torch.stack([u, i], 1).numpy()
+
+
+class BPRBatchSampler:
+    """Vectorised BasicDataset.__getitem__ (dataset.py:119-131): a batch of
+    (user, pos, neg) with user uniform over users that have training items,
+    pos uniform over the user's items, neg uniform over items the user has
+    not interacted with (rejection)."""
+
+    def __init__(self, dataset, batch_size, seed=None):
+        pairs = dataset.train_pairs if hasattr(dataset, 'train_pairs') else \
+            np.asarray(dataset.train_array, np.int64).reshape(-1, 2)
+        self.n_users, self.n_items = dataset.n_users, dataset.n_items
+        self.batch_size = batch_size
+        self.length = len(dataset)
+        order = np.lexsort((pairs[:, 1], pairs[:, 0]))
+        p = pairs[order]
+        self.items = p[:, 1].copy()
+        self.ptr = np.searchsorted(p[:, 0], np.arange(self.n_users + 1))
+        self.deg = np.diff(self.ptr)
+        self.active = np.nonzero(self.deg > 0)[0]
+        self.keys = np.unique(p[:, 0] * self.n_items + p[:, 1])
+        self.rng = np.random.default_rng(seed)
+
+    def __len__(self):
+        return (self.length + self.batch_size - 1) // self.batch_size
+
+    def sample(self, n):
+        users = self.active[self.rng.integers(0, len(self.active), n)]
+        pos = self.items[self.ptr[users] + (self.rng.random(n) * self.deg[users]).astype(np.int64)]
+        neg = self.rng.integers(0, self.n_items, n)
+        bad = self._member(users, neg)
+        while bad.any():
+            neg[bad] = self.rng.integers(0, self.n_items, int(bad.sum()))
+            bad[bad] = self._member(users[bad], neg[bad])
+        return users, pos, neg
+
+    def _member(self, users, items):
+        k = users * self.n_items + items
+        j = np.searchsorted(self.keys, k)
+        j = np.minimum(j, len(self.keys) - 1)
+        return self.keys[j] == k
+
+    def __iter__(self):
+        left = self.length
+        while left > 0:
+            n = min(self.batch_size, left)
+            left -= n
+            yield self.sample(n)

@@ -1,0 +1,206 @@
+"""Graph: a CSR graph resident in HBM plus its row schedule.
+
+Replaces the per-call `dgl.graph((column, row), num_nodes=..., device=...)`
+of the reference (model.py:103-105, 4183, 4194): the structure is built once
+on the host (C++ in libigr, include/igr.h) and kept on the device; only edge
+values change between steps (dropout, anneal).
+
+Layout in HBM:
+    row_ptr  int64[n_rows+1]   col_idx int32[nnz]   edge_id int64[nnz] | None
+    order    int32[n_order]    rows of degree <= split_threshold, heaviest first
+    split_row int32, split_ptr int64, chunk_row int32, chunk_beg int64  (long rows)
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+DEFAULT_SPLIT_THRESHOLD = 512
+DEFAULT_CHUNK_EDGES = 512
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data if a.size else None
+    return a.data_ptr() if a.numel() else None
+
+
+def _np(a, dt):
+    if isinstance(a, torch.Tensor):
+        a = a.detach().cpu().numpy()
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+# ------------------------------------------------------------------ host builders (C++)
+
+def csr_from_coo(row, col, n_rows, n_cols, val=None, dedup=True, n_threads=0, want_eid=True):
+    """COO -> CSR sorted by (row, col).  dedup sums duplicates (scipy .tocsr() +
+    torch .coalesce(), utils.py:33-50); otherwise every edge is kept and
+    `edge_id` maps CSR position -> input edge index (DGL edge id)."""
+    row, col = _np(row, np.int64), _np(col, np.int64)
+    v = None if val is None else _np(val, np.float32)
+    nnz = len(row)
+    row_ptr = np.empty(n_rows + 1, np.int64)
+    col_idx = np.empty(max(nnz, 1), np.int32)
+    val_out = np.empty(max(nnz, 1), np.float32)
+    eid = np.empty(max(nnz, 1), np.int64) if want_eid else None
+    n = ctypes.c_int64(0)
+    L.call('igr_csr_from_coo', n_rows, n_cols, nnz, _ptr(row), _ptr(col), _ptr(v), int(bool(dedup)),
+           _ptr(row_ptr), _ptr(col_idx), _ptr(val_out), _ptr(eid), ctypes.byref(n), n_threads)
+    k = n.value
+    return row_ptr, col_idx[:k].copy(), val_out[:k].copy(), None if eid is None else eid[:k].copy()
+
+
+def csr_transpose(row_ptr, col_idx, n_rows, n_cols, n_threads=0):
+    """Reverse graph: (t_row_ptr, t_col_idx, t_pos) with t_pos = forward CSR position."""
+    row_ptr, col_idx = _np(row_ptr, np.int64), _np(col_idx, np.int32)
+    nnz = int(row_ptr[-1])
+    t_rp = np.empty(n_cols + 1, np.int64)
+    t_ci = np.empty(max(nnz, 1), np.int32)
+    t_pos = np.empty(max(nnz, 1), np.int64)
+    L.call('igr_csr_transpose', n_rows, n_cols, _ptr(row_ptr), _ptr(col_idx), _ptr(t_rp), _ptr(t_ci),
+           _ptr(t_pos), n_threads)
+    return t_rp, t_ci[:nnz], t_pos[:nnz]
+
+
+def row_sums(row_ptr, val=None):
+    row_ptr = _np(row_ptr, np.int64)
+    v = None if val is None else _np(val, np.float32)
+    out = np.empty(len(row_ptr) - 1, np.float32)
+    L.call('igr_csr_row_sums', len(row_ptr) - 1, _ptr(row_ptr), _ptr(v), _ptr(out))
+    return out
+
+
+def sym_norm_values(row_ptr, col_idx, val, dinv, dinv_col=None):
+    """(dinv[r] * val) * dinv_col[c]  (model.py:91-96); dinv_col defaults to dinv."""
+    row_ptr, col_idx = _np(row_ptr, np.int64), _np(col_idx, np.int32)
+    v = None if val is None else _np(val, np.float32)
+    dinv = _np(dinv, np.float32)
+    dc = dinv if dinv_col is None else _np(dinv_col, np.float32)
+    out = np.empty(len(col_idx), np.float32)
+    L.call('igr_sym_norm_values', len(row_ptr) - 1, _ptr(row_ptr), _ptr(col_idx), _ptr(v), _ptr(dinv), _ptr(dc),
+           _ptr(out))
+    return out
+
+
+def plan(row_ptr, split_threshold=DEFAULT_SPLIT_THRESHOLD, chunk_edges=DEFAULT_CHUNK_EDGES):
+    """Degree-binned row schedule (see include/igr.h igr_plan_fill)."""
+    row_ptr = _np(row_ptr, np.int64)
+    n_rows = len(row_ptr) - 1
+    no, ns, nc = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    L.call('igr_plan_size', n_rows, _ptr(row_ptr), split_threshold, chunk_edges,
+           ctypes.byref(no), ctypes.byref(ns), ctypes.byref(nc))
+    order = np.empty(max(no.value, 1), np.int32)
+    split_row = np.empty(max(ns.value, 1), np.int32)
+    split_ptr = np.empty(ns.value + 1, np.int64)
+    chunk_row = np.empty(max(nc.value, 1), np.int32)
+    chunk_beg = np.empty(max(nc.value, 1), np.int64)
+    L.call('igr_plan_fill', n_rows, _ptr(row_ptr), split_threshold, chunk_edges, _ptr(order),
+           _ptr(split_row), _ptr(split_ptr), _ptr(chunk_row), _ptr(chunk_beg))
+    return dict(order=order[:no.value], split_row=split_row[:ns.value], split_ptr=split_ptr,
+                chunk_row=chunk_row[:nc.value], chunk_beg=chunk_beg[:nc.value], chunk_edges=chunk_edges)
+
+
+# ------------------------------------------------------------------ Graph
+
+class Graph:
+    """CSR over destination rows; columns are source nodes.
+
+    `rhs` edge data passed to the ops is indexed by edge id, which equals the
+    CSR position unless `edge_id` is given (DGL multigraph built from an
+    unsorted edge list)."""
+
+    def __init__(self, row_ptr, col_idx, n_rows, n_cols, device='cuda', edge_id=None, symmetric=False,
+                 split_threshold=DEFAULT_SPLIT_THRESHOLD, chunk_edges=DEFAULT_CHUNK_EDGES):
+        row_ptr = _np(row_ptr, np.int64)
+        col_idx = _np(col_idx, np.int32)
+        self.n_rows, self.n_cols = int(n_rows), int(n_cols)
+        assert len(row_ptr) == self.n_rows + 1, 'row_ptr must have n_rows + 1 entries'
+        self.nnz = int(row_ptr[-1])
+        assert len(col_idx) == self.nnz
+        if edge_id is not None:
+            edge_id = _np(edge_id, np.int64)
+            if np.array_equal(edge_id, np.arange(self.nnz, dtype=np.int64)):
+                edge_id = None
+        self.device = torch.device(device)
+        self.symmetric = symmetric
+        self.split_threshold, self.chunk_edges = split_threshold, chunk_edges
+        self._host = dict(row_ptr=row_ptr, col_idx=col_idx, edge_id=edge_id)
+        p = plan(row_ptr, split_threshold, chunk_edges)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)  # noqa: E731
+        self.row_ptr = t(row_ptr)
+        self.col_idx = t(col_idx)
+        self.edge_id = None if edge_id is None else t(edge_id)
+        self.order = t(p['order'])
+        self.split_row = t(p['split_row'])
+        self.split_ptr = t(p['split_ptr'])
+        self.chunk_row = t(p['chunk_row'])
+        self.chunk_beg = t(p['chunk_beg'])
+        self.n_order, self.n_split, self.n_chunks = len(p['order']), len(p['split_row']), len(p['chunk_row'])
+        self.csr = L.IgrCsr(
+            self.n_rows, self.n_cols, self.nnz, _ptr(self.row_ptr), _ptr(self.col_idx), _ptr(self.edge_id),
+            self.n_order, _ptr(self.order), self.n_split, _ptr(self.split_row), _ptr(self.split_ptr),
+            self.n_chunks, _ptr(self.chunk_row), _ptr(self.chunk_beg), chunk_edges)
+        self._reverse = self if symmetric else None
+        self._ws = {}
+        self._edge_rows = None
+
+    # -- constructors
+    @classmethod
+    def from_coo(cls, row, col, n_rows, n_cols, val=None, dedup=True, device='cuda', **kw):
+        """Returns (graph, values-by-edge-id as float32 numpy)."""
+        rp, ci, v, eid = csr_from_coo(row, col, n_rows, n_cols, val, dedup)
+        g = cls(rp, ci, n_rows, n_cols, device=device, edge_id=None if dedup else eid, **kw)
+        if not dedup:
+            # values are addressed by edge id: scatter back to input order
+            vv = np.empty(len(eid), np.float32)
+            vv[eid] = v
+            v = vv
+        return g, v
+
+    def reverse(self):
+        """Reverse graph for gspmm backward; its edge ids are this graph's edge ids."""
+        if self._reverse is None:
+            h = self._host
+            t_rp, t_ci, t_pos = csr_transpose(h['row_ptr'], h['col_idx'], self.n_rows, self.n_cols)
+            eid = t_pos if h['edge_id'] is None else h['edge_id'][t_pos]
+            self._reverse = Graph(t_rp, t_ci, self.n_cols, self.n_rows, device=self.device, edge_id=eid,
+                                  split_threshold=self.split_threshold, chunk_edges=self.chunk_edges)
+            self._reverse._reverse = self
+        return self._reverse
+
+    def workspace(self, d):
+        """Chunk partial sums for split rows (n_chunks * d floats), cached per d."""
+        if self.n_chunks == 0:
+            return None
+        ws = self._ws.get(d)
+        if ws is None:
+            ws = torch.empty(self.n_chunks * d, dtype=torch.float32, device=self.device)
+            self._ws[d] = ws
+        return ws
+
+    def edge_rows(self):
+        """int64[nnz]: destination row of every edge, in edge-id order."""
+        if self._edge_rows is None:
+            h = self._host
+            rows = np.repeat(np.arange(self.n_rows, dtype=np.int64), np.diff(h['row_ptr']))
+            if h['edge_id'] is not None:
+                r2 = np.empty_like(rows)
+                r2[h['edge_id']] = rows
+                rows = r2
+            self._edge_rows = torch.from_numpy(rows).to(self.device)
+        return self._edge_rows
+
+    def host(self):
+        return self._host
+
+    def degrees(self):
+        return np.diff(self._host['row_ptr'])
+
+    def __repr__(self):
+        return (f'Graph(n_rows={self.n_rows}, n_cols={self.n_cols}, nnz={self.nnz}, split_rows={self.n_split}, '
+                f'chunks={self.n_chunks}, device={self.device})')

@@ -1,0 +1,399 @@
+"""igr.model - the reference's model surface on the MI355X path.
+
+Same class names, constructor config dicts and methods as the reference's
+model.py (get_model, BasicModel.predict/save/load, LightGCN, NGCF, IGCN, IMF,
+and the AttIGCN that the reference keeps as dead text at model.py:4223-4287),
+so the reference's trainers and configs drive them unchanged.  The graph
+structure is built once in __init__ (C++ host builder) and lives in HBM;
+every propagation runs through the HIP kernels (igr.ops).
+"""
+import sys
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.nn.init import kaiming_uniform_, normal_, zeros_
+
+from . import ops
+from .graph import Graph, csr_from_coo, row_sums, sym_norm_values
+
+
+def get_model(config, dataset):
+    """model.py:20-25."""
+    config = config.copy()
+    config['dataset'] = dataset
+    model = getattr(sys.modules[__name__], config['name'])
+    return model(config)
+
+
+def init_one_layer(in_features, out_features):
+    """model.py:28-32."""
+    layer = nn.Linear(in_features, out_features)
+    kaiming_uniform_(layer.weight)
+    zeros_(layer.bias)
+    return layer
+
+
+def train_pairs(dataset):
+    """dataset.train_array as an int64 [E, 2] array (reference: list of [u, i])."""
+    ta = getattr(dataset, 'train_pairs', None)
+    if ta is None:
+        ta = np.asarray(dataset.train_array, dtype=np.int64).reshape(-1, 2)
+    return ta
+
+
+def build_norm_adj(n_users, n_items, pairs, device):
+    """utils.generate_daj_mat (utils.py:42-50) + LightGCN.generate_graph (model.py:89-98).
+
+    Returns (Graph marked symmetric, values float32 tensor, degree, dinv).
+    degree = fp32 row sum (duplicates count twice, as scipy sums them);
+    dinv = np.power(max(1, degree), -0.5) in float32 on the host - the same
+    numpy call the reference makes (its SIMD pow is host-ISA dependent, so it
+    is not recomputed on the device); value = (dinv_r * a) * dinv_c."""
+    u, i = pairs[:, 0], pairs[:, 1]
+    n = n_users + n_items
+    row = np.concatenate([u, i + n_users])
+    col = np.concatenate([i + n_users, u])
+    rp, ci, v, _ = csr_from_coo(row, col, n, n, None, dedup=True, want_eid=False)
+    degree = row_sums(rp, v)
+    dinv = np.power(np.maximum(np.float32(1.), degree), np.float32(-0.5)).astype(np.float32)
+    vals = sym_norm_values(rp, ci, v, dinv)
+    g = Graph(rp, ci, n, n, device=device, symmetric=True)
+    return g, torch.from_numpy(vals).to(device), degree, dinv
+
+
+class BasicModel(nn.Module):
+    """model.py:35-53."""
+
+    def __init__(self, model_config):
+        super().__init__()
+        self.config = model_config
+        self.name = model_config['name']
+        self.device = model_config['device']
+        self.n_users = model_config['dataset'].n_users
+        self.n_items = model_config['dataset'].n_items
+        self.trainable = True
+
+    def predict(self, users):
+        raise NotImplementedError
+
+    def save(self, path):
+        torch.save(self.state_dict(), path)
+
+    def load(self, path):
+        self.load_state_dict(torch.load(path, map_location=self.device, weights_only=True))
+
+
+class LightGCN(BasicModel):
+    """model.py:79-127: rep = mean_l A^l E over the symmetric-normalised bipartite graph."""
+
+    def __init__(self, model_config):
+        super().__init__(model_config)
+        self.embedding_size = model_config['embedding_size']
+        self.n_layers = model_config['n_layers']
+        self.embedding = nn.Embedding(self.n_users + self.n_items, self.embedding_size)
+        self.norm_adj, self.norm_vals = self.generate_graph(model_config['dataset'])
+        normal_(self.embedding.weight, std=0.1)
+        self.to(device=self.device)
+
+    def generate_graph(self, dataset):
+        g, vals, self.degree, self.dinv = build_norm_adj(self.n_users, self.n_items, train_pairs(dataset),
+                                                         self.device)
+        return g, vals
+
+    def get_rep(self):
+        """model.py:100-110, fused (one SpMM per layer, running layer mean)."""
+        return ops.propagate(self.norm_adj, self.embedding.weight, self.n_layers, adj_vals=self.norm_vals)
+
+    def bpr_forward(self, users, pos_items, neg_items):
+        rep = self.get_rep()
+        e = self.embedding.weight
+        users_e = ops.gather(e, users)
+        pos_e, neg_e = ops.gather(e, pos_items, self.n_users), ops.gather(e, neg_items, self.n_users)
+        l2_norm_sq = (users_e ** 2).sum(1) + (pos_e ** 2).sum(1) + (neg_e ** 2).sum(1)
+        users_r = ops.gather(rep, users)
+        pos_r, neg_r = ops.gather(rep, pos_items, self.n_users), ops.gather(rep, neg_items, self.n_users)
+        return users_r, pos_r, neg_r, l2_norm_sq
+
+    def predict(self, users, rep=None):
+        rep = self.get_rep() if rep is None else rep
+        users_r = ops.gather(rep, users)
+        return ops.gemm(users_r, rep[self.n_users:])
+
+    def bpr_loss(self, users, pos_items, neg_items):
+        """Fused LightGCN/BPRTrainer step terms: (bpr loss, mean l2 of raw embeddings)."""
+        rep = self.get_rep()
+        bpr, _ = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
+        _, l2 = ops.bpr_loss(self.embedding.weight, users, pos_items, neg_items, 0, self.n_users)
+        return bpr, l2
+
+
+class NGCF(BasicModel):
+    """model.py:3986-4055 (dense d x d layers on the MFMA GEMM)."""
+
+    def __init__(self, model_config):
+        super().__init__(model_config)
+        self.dropout = model_config['dropout']
+        self.embedding_size = model_config['embedding_size']
+        self.layer_sizes = model_config['layer_sizes'].copy()
+        self.embedding = nn.Embedding(self.n_users + self.n_items, self.embedding_size)
+        kaiming_uniform_(self.embedding.weight)
+        self.n_layers = len(self.layer_sizes)
+        self.layer_sizes.insert(0, self.embedding_size)
+        self.gc_layers = nn.ModuleList(
+            [init_one_layer(self.layer_sizes[i - 1], self.layer_sizes[i]) for i in range(1, self.n_layers + 1)])
+        self.bi_layers = nn.ModuleList(
+            [init_one_layer(self.layer_sizes[i - 1], self.layer_sizes[i]) for i in range(1, self.n_layers + 1)])
+        self.norm_adj, self.norm_vals = self.generate_graph(model_config['dataset'])
+        self.to(device=self.device)
+
+    def generate_graph(self, dataset):
+        """adj + I, row-normalised (sklearn normalize l1, model.py:4009-4014)."""
+        pairs = train_pairs(dataset)
+        n = self.n_users + self.n_items
+        u, i = pairs[:, 0], pairs[:, 1]
+        row = np.concatenate([u, i + self.n_users, np.arange(n)])
+        col = np.concatenate([i + self.n_users, u, np.arange(n)])
+        rp, ci, v, _ = csr_from_coo(row, col, n, n, None, dedup=True, want_eid=False)
+        rs = row_sums(rp, v)
+        vals = (v / np.repeat(rs, np.diff(rp))).astype(np.float32)
+        return Graph(rp, ci, n, n, device=self.device), torch.from_numpy(vals).to(self.device)
+
+    def dropout_values(self, vals):
+        return dropout_values(self, vals)
+
+    def get_rep(self):
+        representations = self.embedding.weight
+        all_layer_rep = [representations]
+        vals = self.dropout_values(self.norm_vals)
+        for layer_idx in range(self.n_layers):
+            m0 = ops.gspmm(self.norm_adj, 'mul', 'sum', representations, vals)
+            m1 = representations * m0
+            m0 = ops.linear(m0, self.gc_layers[layer_idx])
+            m1 = ops.linear(m1, self.bi_layers[layer_idx])
+            representations = F.leaky_relu(m0 + m1, negative_slope=0.2)
+            representations = F.dropout(representations, p=self.dropout, training=self.training)
+            all_layer_rep.append(F.normalize(representations, p=2, dim=1))
+        return torch.cat(all_layer_rep, dim=1)
+
+    def bpr_forward(self, users, pos_items, neg_items):
+        """model.py:4046-4052: gathers from rep; l2 over the gathered rep rows."""
+        rep = self.get_rep()
+        users_r = ops.gather(rep, users)
+        pos_r, neg_r = ops.gather(rep, pos_items, self.n_users), ops.gather(rep, neg_items, self.n_users)
+        l2_norm_sq = (users_r ** 2).sum(1) + (pos_r ** 2).sum(1) + (neg_r ** 2).sum(1)
+        return users_r, pos_r, neg_r, l2_norm_sq
+
+    def predict(self, users, rep=None):
+        return LightGCN.predict(self, users, rep)
+
+
+def dropout_values(model, vals):
+    """NGCF.dropout_sp_mat (model.py:4016-4028) as a value mask over the fixed
+    CSR (a dropped edge contributes an exact 0.0).  The uniform draws come
+    from the device generator by default; config['dropout_rng'] = 'cpu' draws
+    them from the CPU generator exactly as the reference does
+    (`torch.rand(nnz).to(device)`), for run-to-run parity with it."""
+    if not model.training or model.dropout == 0:
+        return vals
+    n = vals.numel()
+    if model.config.get('dropout_rng', 'device') == 'cpu':
+        rand = torch.rand(n).to(vals.device)
+    else:
+        rand = torch.rand(n, device=vals.device)
+    return ops.edge_dropout(vals, rand, model.dropout)
+
+
+class IGCN(BasicModel):
+    """model.py:4107-4220: template-feature inductive layer + LightGCN layers."""
+
+    def __init__(self, model_config):
+        super().__init__(model_config)
+        self.embedding_size = model_config['embedding_size']
+        self.n_layers = model_config['n_layers']
+        self.dropout = model_config['dropout']
+        self.feature_ratio = model_config['feature_ratio']
+        self.norm_adj, self.norm_vals = self.generate_graph(model_config['dataset'])
+        self.alpha = 1.
+        self.delta = model_config.get('delta', 0.99)
+        self.feat_mat, self.user_map, self.item_map, self.row_sum = \
+            self.generate_feat(model_config['dataset'], ranking_metric=model_config.get('ranking_metric', 'sort'))
+        self.update_feat_mat()
+        self.embedding = nn.Embedding(self.feat_mat.n_cols, self.embedding_size)
+        self.w = nn.Parameter(torch.ones([self.embedding_size], dtype=torch.float32, device=self.device))
+        normal_(self.embedding.weight, std=0.1)
+        self.to(device=self.device)
+
+    def generate_graph(self, dataset):
+        g, vals, self.degree, self.dinv = build_norm_adj(self.n_users, self.n_items, train_pairs(dataset),
+                                                         self.device)
+        return g, vals
+
+    def update_feat_mat(self):
+        """model.py:4127-4130: value = row_sum[row] ** ((alpha - 1)/2 - 0.5), on the device."""
+        ex = (self.alpha - 1.) / 2. - 0.5
+        self.feat_vals = ops.feat_values(self.feat_mat, self.row_sum, ex)
+
+    def feat_mat_anneal(self):
+        """model.py:4132-4134."""
+        self.alpha *= self.delta
+        self.update_feat_mat()
+
+    def generate_feat(self, dataset, is_updating=False, ranking_metric=None):
+        """model.py:4139-4175, vectorised: user u -> feature U' + item_map[i],
+        item i -> user_map[u], plus one 'general' feature per side; the COO
+        goes through the same duplicate-summing CSR build."""
+        if not is_updating:
+            if self.feature_ratio < 1.:
+                ranked_users, ranked_items = graph_rank_nodes(dataset, ranking_metric)
+                core_users = ranked_users[:int(self.n_users * self.feature_ratio)]
+                core_items = ranked_items[:int(self.n_items * self.feature_ratio)]
+            else:
+                core_users = np.arange(self.n_users, dtype=np.int64)
+                core_items = np.arange(self.n_items, dtype=np.int64)
+            user_map = {int(u): k for k, u in enumerate(core_users)}
+            item_map = {int(i): k for k, i in enumerate(core_items)}
+        else:
+            user_map, item_map = self.user_map, self.item_map
+        umap = np.full(self.n_users, -1, np.int64)
+        imap = np.full(self.n_items, -1, np.int64)
+        if user_map:
+            umap[np.fromiter(user_map.keys(), np.int64)] = np.fromiter(user_map.values(), np.int64)
+        if item_map:
+            imap[np.fromiter(item_map.keys(), np.int64)] = np.fromiter(item_map.values(), np.int64)
+        user_dim, item_dim = len(user_map), len(item_map)
+        pairs = train_pairs(dataset)
+        u, i = pairs[:, 0], pairs[:, 1]
+        ki, ku = imap[i] >= 0, umap[u] >= 0
+        U, I = self.n_users, self.n_items
+        row = np.concatenate([u[ki], U + i[ku], np.arange(U), U + np.arange(I)])
+        col = np.concatenate([user_dim + imap[i[ki]], umap[u[ku]], np.full(U, user_dim + item_dim),
+                              np.full(I, user_dim + item_dim + 1)])
+        n_cols = user_dim + item_dim + 2
+        rp, ci, v, _ = csr_from_coo(row, col, U + I, n_cols, None, dedup=True, want_eid=False)
+        row_sum = torch.from_numpy(row_sums(rp, v)).to(self.device)
+        feat = Graph(rp, ci, U + I, n_cols, device=self.device)
+        return feat, user_map, item_map, row_sum
+
+    def feat_values(self):
+        return dropout_values(self, self.feat_vals)
+
+    def inductive_rep_layer(self, feat_vals):
+        """model.py:4177-4186 (no padding needed: the lhs has n_cols rows)."""
+        return ops.gspmm(self.feat_mat, 'mul', 'sum', self.embedding.weight, feat_vals)
+
+    def get_rep(self):
+        """model.py:4188-4200, fused: inductive SpMM + L layers + layer mean."""
+        return ops.propagate(self.norm_adj, self.embedding.weight, self.n_layers, feat=self.feat_mat,
+                             fvals=self.feat_values(), adj_vals=self.norm_vals)
+
+    def bpr_forward(self, users, pos_items, neg_items):
+        return NGCF.bpr_forward(self, users, pos_items, neg_items)
+
+    def predict(self, users, rep=None):
+        return LightGCN.predict(self, users, rep)
+
+    def bpr_loss(self, users, pos_items, neg_items):
+        """Fused IGCNTrainer terms on rep: (bpr loss, mean l2 of rep rows)."""
+        rep = self.get_rep()
+        return ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
+
+    def aux_loss(self, users, pos_items, neg_items):
+        """IGCNTrainer aux term (trainer.py:542-549) on the raw feature table with w."""
+        loss, _ = ops.bpr_loss(self.embedding.weight, users, pos_items, neg_items, 0, len(self.user_map), w=self.w)
+        return loss
+
+    def save(self, path):
+        """model.py:4208-4211 (key 'sate_dict' kept as in the reference)."""
+        torch.save({'sate_dict': self.state_dict(), 'user_map': self.user_map, 'item_map': self.item_map,
+                    'alpha': self.alpha}, path)
+
+    def load(self, path):
+        """model.py:4213-4220.  Our own checkpoints hold only tensors, ints,
+        floats and dicts, so the restricted loader reads them."""
+        params = torch.load(path, map_location=self.device, weights_only=True)
+        self.load_state_dict(params['sate_dict'])
+        self.user_map = params['user_map']
+        self.item_map = params['item_map']
+        self.alpha = params['alpha']
+        self.feat_mat, _, _, self.row_sum = self.generate_feat(self.config['dataset'], is_updating=True)
+        self.update_feat_mat()
+
+
+class IMF(IGCN):
+    """model.py:4290-4297: the inductive layer alone."""
+
+    def get_rep(self):
+        return ops.propagate(self.norm_adj, self.embedding.weight, 0, feat=self.feat_mat,
+                             fvals=self.feat_values(), adj_vals=self.norm_vals)
+
+
+class AttIGCN(IGCN):
+    """Attention inductive layer (dead text in the reference, model.py:4223-4287).
+
+    x_k = Wk E;  x_q = Wq (F E);  alpha = SDDMM(x_q, x_k) over feat_mat;
+    edge softmax with max-shift, exp(./sqrt(d)/10), head mean; out = SpMM(E, w).
+    The reference detaches E inside the projections (model.py:4258, 4262)."""
+
+    def __init__(self, model_config):
+        BasicModel.__init__(self, model_config)
+        self.embedding_size = model_config['embedding_size']
+        self.n_layers = model_config['n_layers']
+        self.n_heads = model_config.get('n_heads', 4)
+        self.dropout = model_config['dropout']
+        self.feature_ratio = 1.
+        self.alpha = 0.
+        self.delta = model_config.get('delta', 0.99)
+        self.norm_adj, self.norm_vals = self.generate_graph(model_config['dataset'])
+        self.feat_mat, self.user_map, self.item_map, self.row_sum = self.generate_feat(model_config['dataset'])
+        self.update_feat_mat()
+        self.embedding = nn.Embedding(self.feat_mat.n_cols, self.embedding_size)
+        kaiming_uniform_(self.embedding.weight)
+        self.weight_q = init_one_layer(self.embedding_size, self.embedding_size * self.n_heads)
+        self.weight_k = init_one_layer(self.embedding_size, self.embedding_size * self.n_heads)
+        self.w = nn.Parameter(torch.ones([self.embedding_size], dtype=torch.float32, device=self.device))
+        self.to(device=self.device)
+
+    def attention_values(self, feat_vals):
+        e = self.embedding.weight.detach()
+        x_k = ops.linear(e, self.weight_k)
+        x_q = ops.linear(ops.gspmm(self.feat_mat, 'mul', 'sum', e, feat_vals), self.weight_q)
+        alpha = ops.gsddmm(self.feat_mat, 'dot', x_q, x_k, h=self.n_heads)
+        return ops.AttSoftmax.apply(self.feat_mat, alpha, ops.sqrt_scale(self.embedding_size))
+
+    def inductive_rep_layer(self, feat_vals, return_alpha=False):
+        w = self.attention_values(feat_vals)
+        if return_alpha:
+            return w
+        return ops.gspmm(self.feat_mat, 'mul', 'sum', self.embedding.weight, w)
+
+    def get_rep(self):
+        w = self.attention_values(self.feat_values())
+        return ops.propagate(self.norm_adj, self.embedding.weight, self.n_layers, feat=self.feat_mat, fvals=w,
+                             adj_vals=self.norm_vals)
+
+    def bpr_forward(self, users, pos_items, neg_items):
+        users_r, pos_r, neg_r, l2 = NGCF.bpr_forward(self, users, pos_items, neg_items)
+        l2 = l2 + torch.norm(self.weight_q.weight, p=2) ** 2 + torch.norm(self.weight_k.weight, p=2) ** 2
+        return users_r, pos_r, neg_r, l2
+
+
+def graph_rank_nodes(dataset, ranking_metric):
+    """utils.py:186-215 for the 'degree' and 'sort'/'greedy' metrics (feature_ratio < 1)."""
+    pairs = train_pairs(dataset)
+    U, I = dataset.n_users, dataset.n_items
+    u, i = pairs[:, 0], pairs[:, 1]
+    row = np.concatenate([u, i + U])
+    col = np.concatenate([i + U, u])
+    rp, ci, v, _ = csr_from_coo(row, col, U + I, U + I, None, dedup=True, want_eid=False)
+    deg = row_sums(rp, v).astype(np.float64)
+    if ranking_metric == 'degree':
+        metrics = deg
+    elif ranking_metric in ('sort', 'greedy'):
+        # column sums of the l1 row-normalised adjacency (sklearn normalize, utils.py:199-201)
+        rows = np.repeat(np.arange(U + I), np.diff(rp))
+        metrics = np.bincount(ci, weights=v / deg[rows], minlength=U + I)
+    else:
+        raise ValueError(f'ranking metric {ranking_metric} not supported')
+    return np.argsort(metrics[:U])[::-1].copy(), np.argsort(metrics[U:])[::-1].copy()

@@ -1,0 +1,474 @@
+"""igr.ops - device operators of the inductive graph-convolution path.
+
+Thin wrappers over the HIP C ABI (include/igr.h) and the autograd Functions
+built from them.  PyTorch only provides device memory, the current stream
+and autograd bookkeeping; every hot-path byte is moved by the HIP kernels.
+Ops raise IgrError for tensors that are not on a ROCm device (no CPU
+fallback).
+
+DGL-compatible surface (the reference's operator API):
+    graph((src, dst), num_nodes, device)       ~ dgl.graph       model.py:103-105
+    gspmm(g, 'mul', 'sum', lhs, rhs)           ~ dgl.ops.gspmm   model.py:106, 4184, 4196, 4037
+    gspmm(g, 'copy_rhs', 'sum'|'max', None, e) ~ dgl.ops.gspmm   model.py:4270, 4273
+    gsddmm(g, 'dot', lhs, rhs)                 ~ AttIGCN.masked_mm model.py:4246-4255
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .graph import Graph
+
+IgrError = L.IgrError
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not (isinstance(t, torch.Tensor) and t.is_cuda):
+            raise IgrError('igr device ops need tensors on a ROCm (HIP) device; got '
+                           f'{t.device if isinstance(t, torch.Tensor) else type(t)}. There is no CPU fallback.')
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _f32(t):
+    if t.dtype != torch.float32:
+        raise IgrError(f'expected float32, got {t.dtype}')
+    return t
+
+
+def _rows(t):
+    """2-D float32 with unit inner stride; returns (tensor, leading dim)."""
+    _f32(t)
+    if t.dim() != 2:
+        raise IgrError('expected a 2-D tensor')
+    if t.stride(1) != 1 or t.stride(0) < t.shape[1]:
+        t = t.contiguous()
+    return t, t.stride(0)
+
+
+# ------------------------------------------------------------------ raw ops
+
+def epilogue(alpha=1.0, beta=0.0, add=None, acc=None, acc_mode=0, acc_div=1.0, skip_y=False):
+    e = L.IgrEpilogue()
+    e.alpha, e.beta = alpha, beta
+    if add is not None:
+        e.add, e.ld_add = add.data_ptr(), add.stride(0)
+    if acc is not None:
+        e.acc, e.ld_acc = acc.data_ptr(), acc.stride(0)
+    e.acc_mode, e.acc_div, e.skip_y = acc_mode, acc_div, int(skip_y)
+    return e
+
+
+def spmm(g: Graph, x, rhs=None, out=None, epi=None):
+    """y = A x (gspmm 'mul'/'sum'); rhs = edge weights by edge id (None = 1)."""
+    _dev(x, rhs, out)
+    x, ldx = _rows(x)
+    if x.shape[0] < g.n_cols:
+        raise IgrError(f'lhs has {x.shape[0]} rows, graph has {g.n_cols} source nodes')
+    d = x.shape[1]
+    if rhs is not None:
+        _f32(rhs)
+        if rhs.numel() != g.nnz:
+            raise IgrError(f'rhs has {rhs.numel()} values, graph has {g.nnz} edges')
+        rhs = rhs.contiguous()
+    if out is None:
+        out = torch.empty(g.n_rows, d, dtype=torch.float32, device=x.device)
+    if out.shape[0] < g.n_rows or out.shape[1] != d or out.stride(1) != 1:
+        raise IgrError(f'spmm out {tuple(out.shape)} for {g.n_rows} rows x {d}')
+    if out.dtype != torch.float32:
+        raise IgrError('spmm out must be float32')
+    if g.nnz and g.n_rows:
+        ws = g.workspace(d)
+        L.call('igr_spmm_f32', ctypes.byref(g.csr), d, _p(x), ldx, _p(rhs), _p(out), out.stride(0),
+               None if epi is None else ctypes.byref(epi), _p(ws), _stream())
+    elif epi is None or (epi.acc_mode == 0 and not epi.add):
+        out.zero_()
+    else:
+        L.call('igr_spmm_f32', ctypes.byref(g.csr), d, _p(x), ldx, _p(rhs), _p(out), out.stride(0),
+               ctypes.byref(epi), None, _stream())
+    return out
+
+
+def sddmm_dot(g: Graph, u, v, h=1, out=None):
+    """out[eid, j] = <u[row, j, :], v[col, j, :]>; u: [n_rows, h*d], v: [n_cols, h*d]."""
+    _dev(u, v, out)
+    u, ldu = _rows(u.reshape(u.shape[0], -1))
+    v, ldv = _rows(v.reshape(v.shape[0], -1))
+    d = u.shape[1] // h
+    if u.shape[0] < g.n_rows or v.shape[0] < g.n_cols or u.shape[1] != v.shape[1] or d * h != u.shape[1]:
+        raise IgrError(f'sddmm shapes: u {tuple(u.shape)}, v {tuple(v.shape)}, h={h} for graph '
+                       f'{g.n_rows}x{g.n_cols}')
+    if out is None:
+        out = torch.empty(g.nnz, h, dtype=torch.float32, device=u.device)
+    L.call('igr_sddmm_dot_f32', ctypes.byref(g.csr), h, d, _p(u), ldu, _p(v), ldv, _p(out), _stream())
+    return out
+
+
+def segment_reduce(g: Graph, x, reduce='sum'):
+    _dev(x)
+    x = _f32(x).contiguous()
+    h = 1 if x.dim() == 1 else x.shape[1]
+    if x.shape[0] != g.nnz:
+        raise IgrError(f'segment_reduce: {x.shape[0]} edge values for {g.nnz} edges')
+    out = torch.empty(g.n_rows, h, dtype=torch.float32, device=x.device)
+    L.call('igr_segment_reduce_f32', ctypes.byref(g.csr), h, _p(x), 1 if reduce == 'max' else 0, _p(out),
+           _stream())
+    return out if x.dim() > 1 else out[:, 0]
+
+
+def att_softmax(g: Graph, alpha, sqrt_d):
+    _dev(alpha)
+    alpha = _f32(alpha).contiguous()
+    h = alpha.shape[1]
+    if alpha.shape[0] != g.nnz:
+        raise IgrError(f'att_softmax: {alpha.shape[0]} edge rows for {g.nnz} edges')
+    w = torch.empty(g.nnz, dtype=torch.float32, device=alpha.device)
+    rmax = torch.empty(g.n_rows, h, dtype=torch.float32, device=alpha.device)
+    rsum = torch.empty_like(rmax)
+    L.call('igr_att_softmax_f32', ctypes.byref(g.csr), h, _p(alpha), float(sqrt_d), _p(w), _p(rmax), _p(rsum),
+           _stream())
+    return w, rmax, rsum
+
+
+def att_softmax_bwd(g: Graph, alpha, sqrt_d, rmax, rsum, dw):
+    _dev(alpha, dw)
+    dalpha = torch.empty_like(alpha)
+    L.call('igr_att_softmax_bwd_f32', ctypes.byref(g.csr), alpha.shape[1], _p(alpha), float(sqrt_d), _p(rmax),
+           _p(rsum), _p(dw.contiguous()), _p(dalpha), _stream())
+    return dalpha
+
+
+def edge_dropout(val, rand, p, out=None):
+    _dev(val, rand, out)
+    if rand.numel() != val.numel():
+        raise IgrError('edge_dropout: rand and val sizes differ')
+    if out is None:
+        out = torch.empty_like(val)
+    L.call('igr_edge_dropout_f32', val.numel(), _p(val), _p(rand), float(p), _p(out), _stream())
+    return out
+
+
+def feat_values(g: Graph, row_sum, exponent, out=None):
+    _dev(row_sum, out)
+    if row_sum.numel() != g.n_rows:
+        raise IgrError('feat_values: row_sum size differs from n_rows')
+    if out is None:
+        out = torch.empty(g.nnz, dtype=torch.float32, device=row_sum.device)
+    L.call('igr_feat_values_f32', g.n_rows, _p(g.row_ptr), _p(row_sum), float(exponent), _p(out), _stream())
+    return out
+
+
+def gather_rows(src, idx, offset=0):
+    _dev(src, idx)
+    src, lds = _rows(src)
+    idx = idx.to(torch.int64).contiguous()
+    out = torch.empty(idx.numel(), src.shape[1], dtype=torch.float32, device=src.device)
+    L.call('igr_gather_rows_f32', idx.numel(), src.shape[1], _p(idx), int(offset), _p(src), lds, _p(out),
+           out.stride(0), _stream())
+    return out
+
+
+def scatter_add_rows(dst, idx, src, offset=0):
+    _dev(dst, idx, src)
+    src, lds = _rows(src)
+    idx = idx.to(torch.int64).contiguous()
+    L.call('igr_scatter_add_rows_f32', idx.numel(), src.shape[1], _p(idx), int(offset), _p(src), lds, _p(dst),
+           dst.stride(0), _stream())
+    return dst
+
+
+def gemm(a, b, bias=None, trans_a=False, trans_b=False):
+    """C = A(m,k) B(k,n) + bias; b is [n, k] (Linear weight) unless trans_b."""
+    _dev(a, b, bias)
+    a, b = _f32(a).contiguous(), _f32(b).contiguous()
+    m, k = (a.shape[1], a.shape[0]) if trans_a else a.shape
+    n = b.shape[1] if trans_b else b.shape[0]
+    kb = b.shape[0] if trans_b else b.shape[1]
+    if kb != k:
+        raise IgrError(f'gemm inner dims differ: {k} vs {kb}')
+    c = torch.empty(m, n, dtype=torch.float32, device=a.device)
+    L.call('igr_gemm_f32', m, n, k, _p(a), a.stride(0), int(trans_a), _p(b), b.stride(0), int(trans_b),
+           _p(None if bias is None else bias.contiguous()), _p(c), c.stride(0), _stream())
+    return c
+
+
+# ------------------------------------------------------------------ autograd
+
+class GSpMMSum(torch.autograd.Function):
+    """gspmm(g, 'mul', 'sum', x, rhs); backward: dx = A^T dy (reverse graph),
+    drhs[e] = <dy[row_e], x[col_e]> (u_dot_v SDDMM)."""
+
+    @staticmethod
+    def forward(ctx, g, x, rhs):
+        ctx.g = g
+        ctx.save_for_backward(x if (rhs is not None and rhs.requires_grad) else None, rhs)
+        return spmm(g, x, rhs)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, rhs = ctx.saved_tensors
+        g = ctx.g
+        dx = drhs = None
+        dy = dy.contiguous()
+        if ctx.needs_input_grad[1]:
+            dx = spmm(g.reverse(), dy, rhs)
+        if ctx.needs_input_grad[2]:
+            drhs = sddmm_dot(g, dy, x, 1).view(-1)
+        return None, dx, drhs
+
+
+class GSDDMMDot(torch.autograd.Function):
+    """out[e, j] = <u[row_e, j], v[col_e, j]> for h heads; backward are per-head SpMMs."""
+
+    @staticmethod
+    def forward(ctx, g, u, v, h):
+        ctx.g, ctx.h = g, h
+        ctx.save_for_backward(u, v)
+        return sddmm_dot(g, u, v, h)
+
+    @staticmethod
+    def backward(ctx, dout):
+        u, v = ctx.saved_tensors
+        g, h = ctx.g, ctx.h
+        du = dv = None
+        dout = dout.contiguous()
+        d = u.shape[1] // h
+        if ctx.needs_input_grad[1]:
+            du = torch.empty_like(u)
+            for j in range(h):
+                spmm(g, v[:, j * d:(j + 1) * d], dout[:, j].contiguous(), out=du[:, j * d:(j + 1) * d])
+        if ctx.needs_input_grad[2]:
+            dv = torch.empty_like(v)
+            rg = g.reverse()
+            for j in range(h):
+                spmm(rg, u[:, j * d:(j + 1) * d], dout[:, j].contiguous(), out=dv[:, j * d:(j + 1) * d])
+        return None, du, dv, None
+
+
+class SegmentSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, g, x):
+        ctx.g = g
+        return segment_reduce(g, x, 'sum')
+
+    @staticmethod
+    def backward(ctx, dout):
+        g = ctx.g
+        d2 = dout if dout.dim() == 2 else dout[:, None]
+        dx = gather_rows(d2.contiguous(), g.edge_rows())
+        return None, dx if dout.dim() == 2 else dx[:, 0]
+
+
+class AttSoftmax(torch.autograd.Function):
+    """AttIGCN edge softmax + head mean (model.py:4270-4275)."""
+
+    @staticmethod
+    def forward(ctx, g, alpha, sqrt_d):
+        w, rmax, rsum = att_softmax(g, alpha, sqrt_d)
+        ctx.g, ctx.sqrt_d = g, sqrt_d
+        ctx.save_for_backward(alpha, rmax, rsum)
+        return w
+
+    @staticmethod
+    def backward(ctx, dw):
+        alpha, rmax, rsum = ctx.saved_tensors
+        return None, att_softmax_bwd(ctx.g, alpha, ctx.sqrt_d, rmax, rsum, dw), None
+
+
+class Linear(torch.autograd.Function):
+    """nn.Linear on the MFMA GEMM: y = x W^T + b."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return gemm(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = gemm(dy, weight, trans_b=True) if ctx.needs_input_grad[0] else None
+        dw = gemm(dy, x, trans_a=True, trans_b=True) if ctx.needs_input_grad[1] else None
+        db = dy.sum(0) if (ctx.has_bias and ctx.needs_input_grad[2]) else None
+        return dx, dw, db
+
+
+class GatherRows(torch.autograd.Function):
+    """rep[idx + offset] with a scatter-add backward."""
+
+    @staticmethod
+    def forward(ctx, src, idx, offset):
+        ctx.save_for_backward(idx)
+        ctx.n, ctx.offset = src.shape[0], offset
+        return gather_rows(src, idx, offset)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        dsrc = torch.zeros(ctx.n, dy.shape[1], dtype=dy.dtype, device=dy.device)
+        return scatter_add_rows(dsrc, idx, dy, ctx.offset), None, None
+
+
+def linear(x, layer):
+    """Apply an nn.Linear through the MFMA GEMM."""
+    return Linear.apply(x, layer.weight, layer.bias)
+
+
+def gather(src, idx, offset=0):
+    return GatherRows.apply(src, idx, int(offset))
+
+
+class Propagate(torch.autograd.Function):
+    """rep = mean_l(x_l), x_{l+1} = A x_l, x_0 = F emb (inductive) or emb.
+
+    One fused pass per layer: each SpMM's epilogue accumulates the running
+    layer sum, the last one divides by L+1 (model.py:4188-4200, 100-110).
+    Backward (A symmetric => A^T = A bit-exactly for D^-1/2 A D^-1/2):
+        dx_L = g/(L+1);  dx_l = A^T dx_{l+1} + g/(L+1);  demb = F^T dx_0;
+        dfvals[e] = <dx_0[row_e], emb[col_e]> when the feature values need a
+        gradient (AttIGCN's attention weights).
+    """
+
+    @staticmethod
+    def forward(ctx, adj, adj_vals, feat, emb, fvals, n_layers):
+        ctx.adj, ctx.feat, ctx.L = adj, feat, n_layers
+        ctx.save_for_backward(adj_vals, fvals)
+        L1 = n_layers + 1
+        dev = emb.device
+        ctx.emb = emb if (fvals is not None and fvals.requires_grad) else None
+        if feat is not None:
+            x = torch.empty(feat.n_rows, emb.shape[1], dtype=torch.float32, device=dev)
+            if n_layers == 0:
+                return spmm(feat, emb, fvals, out=x)
+            acc = torch.empty_like(x)
+            spmm(feat, emb, fvals, out=x, epi=epilogue(acc=acc, acc_mode=1))
+            own_x = True
+        else:
+            x = emb.contiguous()
+            if n_layers == 0:
+                return x.clone()
+            acc = x.clone()
+            own_x = False  # never write into the caller's embedding table
+        y = torch.empty_like(acc)
+        for layer in range(n_layers):
+            last = layer == n_layers - 1
+            spmm(adj, x, adj_vals, out=y, epi=epilogue(acc=acc, acc_mode=2, acc_div=float(L1) if last else 1.0,
+                                                   skip_y=last))
+            if not last:
+                x, y = y, (x if own_x else torch.empty_like(acc))
+                own_x = True
+        return acc
+
+    @staticmethod
+    def backward(ctx, g):
+        adj_vals, fvals = ctx.saved_tensors
+        adj, feat, n_layers = ctx.adj, ctx.feat, ctx.L
+        L1 = float(n_layers + 1)
+        g = g.contiguous()
+        if n_layers == 0:
+            dx = g
+        else:
+            dx = g / L1
+            at = adj.reverse()
+            nxt = torch.empty_like(dx)
+            for _ in range(n_layers):
+                spmm(at, dx, adj_vals, out=nxt, epi=epilogue(beta=1.0 / L1, add=g))
+                dx, nxt = nxt, dx
+        if feat is None:
+            return None, None, None, dx, None, None
+        demb = spmm(feat.reverse(), dx, fvals) if ctx.needs_input_grad[3] else None
+        dfv = sddmm_dot(feat, dx, emb_saved(ctx), 1).view(-1) if ctx.needs_input_grad[4] else None
+        return None, None, None, demb, dfv, None
+
+
+def emb_saved(ctx):
+    return ctx.emb
+
+
+def propagate(adj, emb, n_layers, feat=None, fvals=None, adj_vals=None):
+    """Fused get_rep: mean over [x0, A x0, ..., A^L x0], x0 = F emb (feat given) or emb."""
+    return Propagate.apply(adj, adj_vals, feat, emb, fvals, n_layers)
+
+
+class BPRLoss(torch.autograd.Function):
+    """Fused BPR term: mean_b softplus(<u, n*w> - <u, p*w>) and mean_b l2_b,
+    rows gathered from one table t (model.py:4046-4052, trainer.py:536-548)."""
+
+    @staticmethod
+    def forward(ctx, t, w, users, pos, neg, off_u, off_i):
+        _dev(t, users, pos, neg, w)
+        t = t.contiguous()
+        B = users.numel()
+        loss = torch.empty(B, dtype=torch.float32, device=t.device)
+        l2 = torch.empty_like(loss)
+        L.call('igr_bpr_fwd_bwd_f32', B, t.shape[1], _p(users), _p(pos), _p(neg), int(off_u), int(off_i), _p(t),
+               t.stride(0), _p(w), _p(loss), _p(l2), 0.0, 0.0, None, 0, None, _stream())
+        ctx.save_for_backward(t, w, users, pos, neg)
+        ctx.off = (int(off_u), int(off_i))
+        return loss.mean(), l2.mean()
+
+    @staticmethod
+    def backward(ctx, g_loss, g_l2):
+        t, w, users, pos, neg = ctx.saved_tensors
+        B = users.numel()
+        gl = float(g_loss) / B if g_loss is not None else 0.0
+        g2 = float(g_l2) / B if g_l2 is not None else 0.0
+        grad = torch.zeros_like(t) if ctx.needs_input_grad[0] else None
+        dw = torch.zeros_like(w) if (w is not None and ctx.needs_input_grad[1]) else None
+        L.call('igr_bpr_fwd_bwd_f32', B, t.shape[1], _p(users), _p(pos), _p(neg), ctx.off[0], ctx.off[1], _p(t),
+               t.stride(0), _p(w), None, None, gl, g2, _p(grad), t.stride(0), _p(dw), _stream())
+        return grad, dw, None, None, None, None, None
+
+
+def bpr_loss(t, users, pos, neg, off_u, off_i, w=None):
+    """Returns (mean softplus BPR loss, mean squared-norm term)."""
+    return BPRLoss.apply(t, w, users.contiguous(), pos.contiguous(), neg.contiguous(), off_u, off_i)
+
+
+# ------------------------------------------------------------------ DGL-compatible API
+
+def graph(edges, num_nodes=None, device='cuda'):
+    """dgl.graph((src, dst), num_nodes=n): rows = dst, columns = src; every
+    edge kept, edge ids = input positions (model.py:104, 4183, 4194)."""
+    src, dst = edges
+    src = src.detach().cpu().numpy() if isinstance(src, torch.Tensor) else np.asarray(src)
+    dst = dst.detach().cpu().numpy() if isinstance(dst, torch.Tensor) else np.asarray(dst)
+    if num_nodes is None:
+        num_nodes = int(max(src.max(initial=-1), dst.max(initial=-1)) + 1)
+    g, _ = Graph.from_coo(dst, src, num_nodes, num_nodes, None, dedup=False, device=device)
+    return g
+
+
+def gspmm(g, op, reduce_op, lhs_data, rhs_data):
+    if op == 'mul' and reduce_op == 'sum':
+        if rhs_data is not None and rhs_data.dim() != 1:
+            raise IgrError('gspmm mul/sum: rhs_data must be one scalar per edge')
+        return GSpMMSum.apply(g, lhs_data, rhs_data)
+    if op == 'copy_rhs' and reduce_op == 'sum':
+        return SegmentSum.apply(g, rhs_data)
+    if op == 'copy_rhs' and reduce_op == 'max':
+        if rhs_data.requires_grad and torch.is_grad_enabled():
+            raise IgrError('gspmm copy_rhs/max backward is not provided; detach the input')
+        return segment_reduce(g, rhs_data, 'max')
+    raise IgrError(f'gspmm op ({op}, {reduce_op}) not supported')
+
+
+def gsddmm(g, op, lhs_data, rhs_data, h=1):
+    """u_dot_v with lhs on destination rows and rhs on source columns."""
+    if op != 'dot':
+        raise IgrError(f'gsddmm op {op} not supported')
+    return GSDDMMDot.apply(g, lhs_data, rhs_data, h)
+
+
+def sqrt_scale(d):
+    return float(np.float32(math.sqrt(d)))

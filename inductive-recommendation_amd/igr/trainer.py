@@ -1,0 +1,265 @@
+"""igr.trainer - the reference's trainer surface (trainer.py) for the path.
+
+BasicTrainer.train / eval / calculate_metrics keep the reference's loop,
+early stopping on NDCG@topks[4], checkpoint naming and metric definitions
+(trainer.py:25-210).  BPRTrainer and IGCNTrainer keep the per-batch loss
+math (trainer.py:403-429, 518-561); by default the loss terms go through the
+fused HIP BPR kernel (model.bpr_loss / aux_loss), and `fused: False` in the
+trainer config runs the reference's exact op sequence on bpr_forward.
+Evaluation computes the representation once per eval instead of once per
+512-user batch (the reference's predict re-propagates, model.py:123); in
+eval mode both are the same function of the weights.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch.optim import SGD, Adam  # noqa: F401  (resolved by name, trainer.py:44-46)
+
+from .dataset import AuxiliaryDataset, BPRBatchSampler
+from .utils import AverageMeter
+
+
+def get_trainer(config, dataset, model):
+    """trainer.py:16-22."""
+    config = config.copy()
+    config['dataset'] = dataset
+    config['model'] = model
+    trainer = getattr(sys.modules[__name__], config['name'])
+    return trainer(config)
+
+
+def calculate_metrics(eval_data, rec_items, topks):
+    """trainer.py:115-144, vectorised: Precision/Recall/NDCG@k averaged over
+    users with a non-empty eval set."""
+    n_users, kmax = rec_items.shape
+    lens = np.array([len(x) for x in eval_data], dtype=np.int32)
+    ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    flat = np.fromiter((i for x in eval_data for i in x), dtype=np.int64, count=int(ptr[-1]))
+    n_items = int(max(rec_items.max(initial=0), flat.max(initial=0)) + 1)
+    ev_keys = np.unique(np.repeat(np.arange(n_users, dtype=np.int64), lens) * n_items + flat)
+    rk = (np.arange(n_users, dtype=np.int64)[:, None] * n_items + rec_items).ravel()
+    j = np.minimum(np.searchsorted(ev_keys, rk), max(len(ev_keys) - 1, 0))
+    hit = (ev_keys[j] == rk).reshape(n_users, kmax).astype(np.float32) if len(ev_keys) else \
+        np.zeros((n_users, kmax), np.float32)
+    res = {'Precision': {}, 'Recall': {}, 'NDCG': {}}
+    for k in topks:
+        hit_num = hit[:, :k].sum(1)
+        with np.errstate(invalid='ignore', divide='ignore'):
+            recalls = hit_num / lens
+        max_hit = np.minimum(lens, k)
+        max_hit_matrix = (np.arange(k)[None, :] < max_hit[:, None]).astype(np.float32)
+        den = np.log2(np.arange(2, k + 2, dtype=np.float32))[None, :]
+        dcg = (hit[:, :k] / den).sum(1)
+        idcg = (max_hit_matrix / den).sum(1)
+        with np.errstate(invalid='ignore', divide='ignore'):
+            ndcg = dcg / idcg
+        m = max_hit > 0
+        res['Precision'][k] = (hit_num / k)[m].mean()
+        res['Recall'][k] = recalls[m].mean()
+        res['NDCG'][k] = ndcg[m].mean()
+    return res
+
+
+def _csr(lists, n):
+    lens = np.array([len(x) for x in lists[:n]], dtype=np.int64)
+    ptr = np.concatenate([[0], np.cumsum(lens)])
+    flat = np.fromiter((i for x in lists[:n] for i in x), dtype=np.int64, count=int(ptr[-1]))
+    return ptr, flat
+
+
+class BasicTrainer:
+    """trainer.py:25-253."""
+
+    def __init__(self, trainer_config):
+        self.config = trainer_config
+        self.name = trainer_config['name']
+        self.dataset = trainer_config['dataset']
+        self.model = trainer_config['model']
+        self.topks = trainer_config['topks']
+        self.device = trainer_config['device']
+        self.n_epochs = trainer_config['n_epochs']
+        self.max_patience = trainer_config.get('max_patience', 50)
+        self.val_interval = trainer_config.get('val_interval', 1)
+        self.test_batch_size = trainer_config['test_batch_size']
+        self.epoch = 0
+        self.best_ndcg = -np.inf
+        self.save_path = None
+        self.opt = None
+        self.verbose = trainer_config.get('verbose', True)
+
+    def initialize_optimizer(self):
+        opt = getattr(sys.modules[__name__], self.config['optimizer'])
+        self.opt = opt(self.model.parameters(), lr=self.config['lr'])
+
+    def train_one_epoch(self):
+        raise NotImplementedError
+
+    def train(self, verbose=True, writer=None):
+        """trainer.py:58-113."""
+        if not self.model.trainable:
+            _, metrics = self.eval('val')
+            return metrics['NDCG'][self.topks[5]]
+        ckpt_dir = self.config.get('checkpoint_dir', 'checkpoints')
+        os.makedirs(ckpt_dir, exist_ok=True)
+        patience = self.max_patience
+        for self.epoch in range(self.n_epochs):
+            start = time.time()
+            self.model.train()
+            loss = self.train_one_epoch()
+            _, metrics = self.eval('train')
+            if verbose:
+                print('Epoch {:d}/{:d}, Loss: {:.6f}, Time: {:.3f}s'.format(self.epoch, self.n_epochs, loss,
+                                                                          time.time() - start))
+            if writer:
+                writer.add_scalar('{:s}_{:s}/train_loss'.format(self.model.name, self.name), loss, self.epoch)
+            if (self.epoch + 1) % self.val_interval != 0:
+                continue
+            start = time.time()
+            results, metrics = self.eval('val')
+            if verbose:
+                print('Validation result. {:s}Time: {:.3f}s'.format(results, time.time() - start))
+            ndcg = metrics['NDCG'][self.topks[4]]
+            if ndcg > self.best_ndcg:
+                if self.save_path and os.path.exists(self.save_path):
+                    os.remove(self.save_path)
+                self.save_path = os.path.join(ckpt_dir, '{:s}_{:s}_{:s}_{:.3f}.pth'.format(
+                    self.model.name, self.name, self.dataset.name, ndcg * 100))
+                self.best_ndcg = ndcg
+                self.model.save(self.save_path)
+                patience = self.max_patience
+                if verbose:
+                    print('Best NDCG, save model to {:s}'.format(self.save_path))
+            else:
+                patience -= self.val_interval
+                if patience <= 0:
+                    if verbose:
+                        print('Early stopping!')
+                    break
+        if self.save_path:
+            self.model.load(self.save_path)
+        return self.best_ndcg
+
+    def calculate_metrics(self, eval_data, rec_items):
+        return calculate_metrics(eval_data, rec_items, self.topks)
+
+    @torch.no_grad()
+    def rank(self, val_or_test, banned_items=None):
+        """Top-max(topks) items per user, train items (and val items for
+        'test') excluded except for split 'train' (trainer.py:146-170)."""
+        self.model.eval()
+        n_users = self.dataset.n_users
+        rep = self.model.get_rep()
+        excl = None
+        if val_or_test != 'train':
+            lists = self.dataset.train_data
+            if val_or_test == 'test':
+                lists = [a + b for a, b in zip(self.dataset.train_data, self.dataset.val_data)]
+            excl = _csr(lists, n_users)
+        kmax = max(self.topks)
+        rec = []
+        for s in range(0, n_users, self.test_batch_size):
+            e = min(n_users, s + self.test_batch_size)
+            users = torch.arange(s, e, dtype=torch.int64, device=self.device)
+            scores = self.model.predict(users, rep)
+            if excl is not None:
+                ptr, flat = excl
+                cnt = np.diff(ptr[s:e + 1])
+                r = torch.from_numpy(np.repeat(np.arange(e - s), cnt)).to(self.device)
+                c = torch.from_numpy(flat[ptr[s]:ptr[e]]).to(self.device)
+                scores[r, c] = -np.inf
+            if banned_items is not None:
+                scores[:, torch.as_tensor(banned_items, device=self.device)] = -np.inf
+            _, items = torch.topk(scores, k=kmax)
+            rec.append(items.cpu().numpy())
+        return np.concatenate(rec, axis=0)
+
+    def eval(self, val_or_test, banned_items=None):
+        """trainer.py:146-210; returns (result string, metrics)."""
+        eval_data = getattr(self.dataset, val_or_test + '_data')
+        rec_items = self.rank(val_or_test, banned_items)
+        metrics = self.calculate_metrics(eval_data, rec_items)
+        fmt = lambda m: ''.join('{:.3f}, '.format(metrics[m][k] * 100.) for k in self.topks)  # noqa: E731
+        results = 'Precision: {:s}Recall: {:s}NDCG: {:s}'.format(fmt('Precision'), fmt('Recall'), fmt('NDCG'))
+        return results, metrics
+
+
+class BPRTrainer(BasicTrainer):
+    """trainer.py:403-429."""
+
+    def __init__(self, trainer_config):
+        super().__init__(trainer_config)
+        self.sampler = BPRBatchSampler(self.dataset, trainer_config['batch_size'], trainer_config.get('seed'))
+        self.initialize_optimizer()
+        self.l2_reg = trainer_config['l2_reg']
+        self.fused = trainer_config.get('fused', True)
+
+    def step(self, users, pos_items, neg_items):
+        """One training step on a device batch; returns the loss tensor."""
+        if self.fused and hasattr(self.model, 'bpr_loss'):
+            bpr_loss, l2 = self.model.bpr_loss(users, pos_items, neg_items)
+            loss = bpr_loss + self.l2_reg * l2
+        else:
+            users_r, pos_r, neg_r, l2_norm_sq = self.model.bpr_forward(users, pos_items, neg_items)
+            pos_scores = torch.sum(users_r * pos_r, dim=1)
+            neg_scores = torch.sum(users_r * neg_r, dim=1)
+            loss = F.softplus(neg_scores - pos_scores).mean() + self.l2_reg * l2_norm_sq.mean()
+        self.opt.zero_grad()
+        loss.backward()
+        self.opt.step()
+        return loss
+
+    def train_one_epoch(self):
+        losses = AverageMeter()
+        for u, p, n in self.sampler:
+            t = lambda a: torch.from_numpy(a).to(self.device)  # noqa: E731
+            loss = self.step(t(u), t(p), t(n))
+            losses.update(loss.item(), len(u))
+        return losses.avg
+
+
+class IGCNTrainer(BasicTrainer):
+    """trainer.py:518-561: BPR on rep + l2 + aux BPR on the raw feature table (with w)."""
+
+    def __init__(self, trainer_config):
+        super().__init__(trainer_config)
+        bs = trainer_config['batch_size']
+        seed = trainer_config.get('seed')
+        self.sampler = BPRBatchSampler(self.dataset, bs, seed)
+        self.aux_sampler = BPRBatchSampler(AuxiliaryDataset(self.dataset, self.model.user_map, self.model.item_map),
+                                           bs, None if seed is None else seed + 1)
+        self.initialize_optimizer()
+        self.l2_reg = trainer_config['l2_reg']
+        self.aux_reg = trainer_config['aux_reg']
+        self.fused = trainer_config.get('fused', True)
+
+    def step(self, users, pos_items, neg_items, a_users, a_pos, a_neg):
+        m = self.model
+        if self.fused:
+            bpr_loss, l2 = m.bpr_loss(users, pos_items, neg_items)
+            aux_loss = m.aux_loss(a_users, a_pos, a_neg)
+        else:
+            users_r, pos_r, neg_r, l2_norm_sq = m.bpr_forward(users, pos_items, neg_items)
+            bpr_loss = F.softplus(torch.sum(users_r * neg_r, 1) - torch.sum(users_r * pos_r, 1)).mean()
+            l2 = l2_norm_sq.mean()
+            ue = m.embedding(a_users)
+            pe = m.embedding(a_pos + len(m.user_map))
+            ne = m.embedding(a_neg + len(m.user_map))
+            aux_loss = F.softplus(torch.sum(ue * ne * m.w[None, :], 1) - torch.sum(ue * pe * m.w[None, :], 1)).mean()
+        loss = bpr_loss + self.l2_reg * l2 + self.aux_reg * aux_loss
+        self.opt.zero_grad()
+        loss.backward()
+        self.opt.step()
+        return loss
+
+    def train_one_epoch(self):
+        losses = AverageMeter()
+        t = lambda a: torch.from_numpy(a).to(self.device)  # noqa: E731
+        for (u, p, n), (au, ap, an) in zip(self.sampler, self.aux_sampler):
+            loss = self.step(t(u), t(p), t(n), t(au), t(ap), t(an))
+            losses.update(loss.item(), len(au))
+        self.model.feat_mat_anneal()
+        return losses.avg

@@ -1,0 +1,132 @@
+"""C-ABI library (CPU-side): loads, exports every declared symbol, and its host
+graph builders match the oracle / golden fixtures bit-exactly."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+from igr import _lib
+from igr import graph as G
+from igr import model as M
+from igr import ops
+from oracle import igr_oracle as O
+
+
+def declared_symbols():
+    txt = open(os.path.join(ROOT, 'include', 'igr.h')).read()
+    txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
+    return sorted(set(re.findall(r'\b(igr_[a-z0-9_]+)\s*\(', txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), f'{s} declared in include/igr.h but not exported'
+    assert set(syms) == set(_lib.SIGNATURES), 'ctypes binding out of sync with include/igr.h'
+    assert lib.igr_version() == 10000
+
+
+def test_error_path_reports_message():
+    with pytest.raises(_lib.IgrError, match='index out of range'):
+        G.csr_from_coo(np.array([0, 5]), np.array([0, 0]), 3, 3)
+    n = ctypes.c_int64()
+    with pytest.raises(_lib.IgrError, match='chunk_edges'):
+        _lib.call('igr_plan_size', 1, np.array([0, 1], np.int64).ctypes.data, 4, 100, ctypes.byref(n),
+                  ctypes.byref(n), ctypes.byref(n))
+
+
+def test_device_ops_refuse_cpu_tensors():
+    rp, ci, v, _ = G.csr_from_coo(np.array([0, 1]), np.array([1, 0]), 2, 2)
+    g = G.Graph(rp, ci, 2, 2, device='cpu')
+    with pytest.raises(_lib.IgrError, match='no CPU fallback'):
+        ops.spmm(g, torch.ones(2, 4))
+
+
+@pytest.mark.parametrize('dedup', [True, False])
+def test_csr_from_coo_matches_oracle(dedup):
+    rng = np.random.default_rng(1)
+    n_rows, n_cols, nnz = 300, 200, 5000
+    row, col = rng.integers(0, n_rows, nnz), rng.integers(0, n_cols, nnz)
+    val = rng.random(nnz).astype(np.float32)
+    rp, ci, v, eid = G.csr_from_coo(row, col, n_rows, n_cols, val, dedup)
+    ref = O.coo_to_csr(n_rows, n_cols, row, col, val, dedup)
+    np.testing.assert_array_equal(rp, ref.row_ptr)
+    np.testing.assert_array_equal(ci, ref.col)
+    np.testing.assert_array_equal(v, ref.val)
+    np.testing.assert_array_equal(eid, ref.eid)
+
+
+def test_csr_transpose_matches_oracle():
+    rng = np.random.default_rng(2)
+    row, col = rng.integers(0, 50, 900), rng.integers(0, 70, 900)
+    rp, ci, v, _ = G.csr_from_coo(row, col, 50, 70, None, True)
+    t_rp, t_ci, t_pos = G.csr_transpose(rp, ci, 50, 70)
+    A = O.CSR(50, 70, rp, ci.astype(np.int64), v)
+    T = A.transpose()
+    np.testing.assert_array_equal(t_rp, T.row_ptr)
+    np.testing.assert_array_equal(t_ci, T.col)
+    np.testing.assert_array_equal(t_pos, T.eid)
+
+
+def test_plan_covers_rows_heaviest_first():
+    rng = np.random.default_rng(3)
+    deg = np.concatenate([rng.integers(0, 40, 500), [0, 0, 2000, 700, 5000, 513, 512]])
+    rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    p = G.plan(rp, split_threshold=512, chunk_edges=256)
+    order, sr, sp, cr, cb = p['order'], p['split_row'], p['split_ptr'], p['chunk_row'], p['chunk_beg']
+    assert sorted(np.concatenate([order, sr]).tolist()) == list(range(len(deg)))
+    assert np.all(deg[order] <= 512) and np.all(deg[sr] > 512)
+    assert np.all(np.diff(deg[order]) <= 0) and np.all(np.diff(deg[sr]) <= 0)
+    for s, r in enumerate(sr):
+        chunks = list(range(sp[s], sp[s + 1]))
+        assert all(cr[c] == r for c in chunks)
+        np.testing.assert_array_equal(cb[chunks], np.arange(rp[r], rp[r + 1], 256))
+
+
+def test_norm_adj_host_build_bit_exact(golden):
+    nu, ni = int(golden['n_users']), int(golden['n_items'])
+    g, vals, deg, dinv = M.build_norm_adj(nu, ni, golden['train_array'], 'cpu')
+    h = g.host()
+    np.testing.assert_array_equal(np.repeat(np.arange(nu + ni), np.diff(h['row_ptr'])), golden['norm_idx'][0])
+    np.testing.assert_array_equal(h['col_idx'], golden['norm_idx'][1])
+    np.testing.assert_array_equal(deg, golden['degree'])
+    np.testing.assert_array_equal(dinv, golden['dinv'])
+    np.testing.assert_array_equal(vals.numpy(), golden['norm_val'])
+
+
+def test_feat_structure_bit_exact(golden):
+    nu, ni = int(golden['n_users']), int(golden['n_items'])
+    ta = golden['train_array']
+    F = O.generate_feat(nu, ni, ta)
+    U, I = nu, ni
+    u, i = ta[:, 0], ta[:, 1]
+    row = np.concatenate([u, U + i, np.arange(U), U + np.arange(I)])
+    col = np.concatenate([U + i, u, np.full(U, U + I), np.full(I, U + I + 1)])
+    rp, ci, v, _ = G.csr_from_coo(row, col, U + I, U + I + 2, None, True)
+    np.testing.assert_array_equal(np.repeat(np.arange(U + I), np.diff(rp)), golden['feat_idx'][0])
+    np.testing.assert_array_equal(ci, golden['feat_idx'][1])
+    np.testing.assert_array_equal(G.row_sums(rp, v), golden['row_sum'])
+    np.testing.assert_array_equal(G.row_sums(rp, v), F.row_sum)
+
+
+def test_reverse_graph_edge_ids():
+    rng = np.random.default_rng(4)
+    src, dst = rng.integers(0, 30, 400), rng.integers(0, 20, 400)
+    g = ops.graph((torch.from_numpy(src), torch.from_numpy(dst)), num_nodes=30, device='cpu')
+    h = g.host()
+    assert h['edge_id'] is not None
+    rows = np.repeat(np.arange(30), np.diff(h['row_ptr']))
+    # CSR position p holds input edge edge_id[p]: dst == row, src == col
+    np.testing.assert_array_equal(dst[h['edge_id']], rows)
+    np.testing.assert_array_equal(src[h['edge_id']], h['col_idx'])
+    r = g.reverse()
+    rh = r.host()
+    rrows = np.repeat(np.arange(30), np.diff(rh['row_ptr']))
+    np.testing.assert_array_equal(src[rh['edge_id']], rrows)
+    np.testing.assert_array_equal(dst[rh['edge_id']], rh['col_idx'])

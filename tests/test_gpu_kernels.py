@@ -1,0 +1,223 @@
+"""GPU parity of the HIP kernels against the CPU oracle (through the C ABI).
+
+Tolerance (fp32): |y - y64| <= 1e-5 |y64| + 1e-6 max|y64_row|
+against a float64 oracle; integer / index outputs bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from igr import graph as G
+from igr import ops
+from oracle import igr_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+RTOL, ATOL_ROW = 1e-5, 1e-6
+
+
+def close(y, ref, rtol=RTOL, atol_row=ATOL_ROW):
+    y = np.asarray(y, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert y.shape == ref.shape, (y.shape, ref.shape)
+    if ref.size == 0:
+        return
+    rowmax = np.abs(ref).max(axis=-1, keepdims=True) if ref.ndim > 1 else np.abs(ref).max()
+    err = np.abs(y - ref)
+    bound = rtol * np.abs(ref) + atol_row * rowmax + 1e-30
+    worst = float((err / bound).max())
+    assert worst <= 1.0, f'max err/bound {worst:.3g}, max abs err {err.max():.3g}'
+
+
+def rand_graph(n_rows, n_cols, nnz, seed, skew=False, dedup=True, **kw):
+    rng = np.random.default_rng(seed)
+    if skew:
+        w = 1.0 / np.arange(1, n_rows + 1) ** 1.2
+        row = rng.choice(n_rows, nnz, p=w / w.sum())
+    else:
+        row = rng.integers(0, n_rows, nnz)
+    col = rng.integers(0, n_cols, nnz)
+    val = rng.standard_normal(nnz).astype(np.float32)
+    g, v = G.Graph.from_coo(row, col, n_rows, n_cols, val, dedup=dedup, device=DEV, **kw)
+    return g, v
+
+
+def oracle_csr(g, v):
+    h = g.host()
+    eid = h['edge_id']
+    vv = v if eid is None else v[eid]
+    return O.CSR(g.n_rows, g.n_cols, h['row_ptr'], h['col_idx'].astype(np.int64), vv)
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+@pytest.mark.parametrize('d', [32, 64, 128, 256, 48, 20])
+@pytest.mark.parametrize('skew', [False, True])
+def test_spmm_matches_oracle(d, skew):
+    g, v = rand_graph(700, 500, 20000, seed=d, skew=skew, split_threshold=64, chunk_edges=64)
+    if skew:
+        assert g.n_split > 0 and g.n_chunks > g.n_split  # exercises the chunk tier + combine
+    x = np.random.default_rng(9).standard_normal((500, d)).astype(np.float32)
+    y = ops.spmm(g, t(x), t(v)).cpu().numpy()
+    close(y, O.spmm64(oracle_csr(g, v), x))
+
+
+def test_spmm_unit_weights_and_empty_rows():
+    g, v = rand_graph(300, 100, 150, seed=5)  # most rows empty
+    x = np.random.default_rng(1).standard_normal((100, 64)).astype(np.float32)
+    y = ops.spmm(g, t(x)).cpu().numpy()
+    A = oracle_csr(g, v)
+    A.val = np.ones_like(A.val)
+    close(y, O.spmm64(A, x))
+    assert np.all(y[np.diff(g.host()['row_ptr']) == 0] == 0)
+
+
+def test_spmm_multigraph_edge_ids():
+    """DGL semantics: rhs indexed by input edge id, duplicate edges kept."""
+    g, v = rand_graph(200, 150, 6000, seed=7, dedup=False, split_threshold=64, chunk_edges=64)
+    assert g.edge_id is not None
+    x = np.random.default_rng(2).standard_normal((150, 64)).astype(np.float32)
+    y = ops.spmm(g, t(x), t(v)).cpu().numpy()
+    close(y, O.spmm64(oracle_csr(g, v), x))
+
+
+def test_spmm_strided_lhs_and_epilogues():
+    g, v = rand_graph(400, 400, 9000, seed=11, split_threshold=64, chunk_edges=64)
+    rng = np.random.default_rng(3)
+    big = rng.standard_normal((400, 96)).astype(np.float32)
+    x = t(big)[:, 16:80]  # leading dim 96, 16-B aligned offset
+    add = rng.standard_normal((400, 64)).astype(np.float32)
+    acc0 = rng.standard_normal((400, 64)).astype(np.float32)
+    ref = O.spmm64(oracle_csr(g, v), np.ascontiguousarray(big[:, 16:80]))
+    acc = t(acc0)
+    y = ops.spmm(g, x, t(v), epi=ops.epilogue(alpha=0.5, beta=2.0, add=t(add), acc=acc, acc_mode=2, acc_div=3.0))
+    yr = 0.5 * ref + 2.0 * add
+    close(y.cpu().numpy(), yr, atol_row=2e-6)
+    close(acc.cpu().numpy(), (acc0 + yr) / 3.0, atol_row=2e-6)
+    acc2 = torch.empty_like(acc)
+    ops.spmm(g, x, t(v), out=torch.empty_like(acc), epi=ops.epilogue(acc=acc2, acc_mode=1, skip_y=True))
+    close(acc2.cpu().numpy(), ref)
+
+
+def test_spmm_deterministic():
+    g, v = rand_graph(500, 500, 40000, seed=13, skew=True, split_threshold=64, chunk_edges=64)
+    x = t(np.random.default_rng(4).standard_normal((500, 64)).astype(np.float32))
+    a = ops.spmm(g, x, t(v))
+    for _ in range(3):
+        assert torch.equal(a, ops.spmm(g, x, t(v)))
+
+
+def test_spmm_linearity_large():
+    """Size-independent property at 1M edges: A(x1 + 2 x2) = A x1 + 2 A x2."""
+    g, v = rand_graph(200000, 50000, 1000000, seed=17)
+    rng = np.random.default_rng(5)
+    x1 = t(rng.standard_normal((50000, 64)).astype(np.float32))
+    x2 = t(rng.standard_normal((50000, 64)).astype(np.float32))
+    vv = t(v)
+    lhs = ops.spmm(g, x1 + 2 * x2, vv).double()
+    rhs = ops.spmm(g, x1, vv).double() + 2 * ops.spmm(g, x2, vv).double()
+    scale = ops.spmm(g, x1.abs() + 2 * x2.abs(), vv.abs()).double()
+    assert float(((lhs - rhs).abs() - 1e-5 * scale).max()) <= 0
+    # spot rows against the float64 oracle
+    A = oracle_csr(g, v)
+    rows = np.random.default_rng(6).choice(g.n_rows, 64, replace=False)
+    y = ops.spmm(g, x1, vv).cpu().numpy()[rows]
+    xs = x1.cpu().numpy()
+    ref = np.stack([(A.val[A.row_ptr[r]:A.row_ptr[r + 1], None].astype(np.float64)
+                     * xs[A.col[A.row_ptr[r]:A.row_ptr[r + 1]]]).sum(0) for r in rows])
+    close(y, ref)
+
+
+def test_sddmm_and_segment_reduce():
+    g, v = rand_graph(300, 250, 6000, seed=19, dedup=False)
+    rng = np.random.default_rng(7)
+    for h, d in [(4, 32), (4, 64), (1, 64), (2, 24)]:
+        q = rng.standard_normal((300, h * d)).astype(np.float32)
+        k = rng.standard_normal((250, h * d)).astype(np.float32)
+        out = ops.sddmm_dot(g, t(q), t(k), h).cpu().numpy()
+        A = oracle_csr(g, v)
+        ref = O.sddmm_dot(A, q.reshape(300, h, d), k.reshape(250, h, d))
+        eid = g.host()['edge_id']
+        close(out[eid], ref, rtol=2e-5)
+    x = rng.standard_normal((g.nnz, 3)).astype(np.float32)
+    A = oracle_csr(g, v)
+    eid = g.host()['edge_id']
+    for red in ['sum', 'max']:
+        y = ops.segment_reduce(g, t(x), red).cpu().numpy()
+        close(y, O.segment_reduce(A, x[eid], red), rtol=2e-5)
+
+
+def test_att_softmax_forward_backward():
+    g, v = rand_graph(200, 180, 4000, seed=23, skew=True)
+    rng = np.random.default_rng(8)
+    alpha = (rng.standard_normal((g.nnz, 4)) * 30).astype(np.float32)
+    sd = ops.sqrt_scale(32)
+    w = ops.att_softmax(g, t(alpha), sd)[0].cpu().numpy()
+    close(w, O.att_softmax(oracle_csr(g, v), alpha, 32), rtol=2e-5)
+    # backward against torch float64 autograd of the reference expression (model.py:4270-4275)
+    a = t(alpha).requires_grad_(True)
+    dw = t(rng.standard_normal(g.nnz).astype(np.float32))
+    ops.AttSoftmax.apply(g, a, sd).backward(dw)
+    a64 = torch.tensor(alpha, dtype=torch.float64, requires_grad=True)
+    rows = torch.from_numpy(np.repeat(np.arange(g.n_rows), np.diff(g.host()['row_ptr'])))
+    m = torch.zeros(g.n_rows, 4, dtype=torch.float64).scatter_reduce(0, rows[:, None].expand(-1, 4), a64.detach(),
+                                                                     'amax', include_self=False)
+    z = torch.exp((a64 - m[rows]) / sd / 10.)
+    s = torch.zeros(g.n_rows, 4, dtype=torch.float64).index_add(0, rows, z)
+    (z / s[rows]).mean(-1).backward(dw.cpu().double())
+    close(a.grad.cpu().numpy(), a64.grad.numpy(), rtol=1e-4, atol_row=1e-5)
+
+
+def test_gemm_mfma_matches_torch():
+    rng = np.random.default_rng(9)
+    for (m, n, k) in [(1000, 256, 64), (77, 64, 64), (130, 33, 17)]:
+        a = rng.standard_normal((m, k)).astype(np.float32)
+        w = rng.standard_normal((n, k)).astype(np.float32)
+        b = rng.standard_normal(n).astype(np.float32)
+        c = ops.gemm(t(a), t(w), t(b)).cpu().numpy()
+        close(c, a.astype(np.float64) @ w.T.astype(np.float64) + b, rtol=1e-5, atol_row=1e-5)
+        ct = ops.gemm(t(a.T.copy()), t(w.T.copy()), None, trans_a=True, trans_b=True).cpu().numpy()
+        close(ct, a.astype(np.float64) @ w.T.astype(np.float64), rtol=1e-5, atol_row=1e-5)
+
+
+def test_gather_scatter_and_bpr():
+    rng = np.random.default_rng(10)
+    T = rng.standard_normal((500, 64)).astype(np.float32)
+    w = rng.random(64).astype(np.float32) + 0.5
+    users, pos, neg = rng.integers(0, 200, 256), rng.integers(0, 300, 256), rng.integers(0, 300, 256)
+    g = ops.gather_rows(t(T), t(pos), 200).cpu().numpy()
+    np.testing.assert_array_equal(g, T[200 + pos])
+    tt = t(T).requires_grad_(True)
+    ww = t(w).requires_grad_(True)
+    loss, l2 = ops.bpr_loss(tt, t(users), t(pos), t(neg), 0, 200, w=ww)
+    (loss + 0.3 * l2).backward()
+    T64 = torch.tensor(T, dtype=torch.float64, requires_grad=True)
+    w64 = torch.tensor(w, dtype=torch.float64, requires_grad=True)
+    u, p, n = T64[users], T64[200 + pos], T64[200 + neg]
+    s = (u * n * w64).sum(1) - (u * p * w64).sum(1)
+    rl = torch.nn.functional.softplus(s).mean()
+    r2 = ((u ** 2).sum(1) + (p ** 2).sum(1) + (n ** 2).sum(1)).mean()
+    (rl + 0.3 * r2).backward()
+    np.testing.assert_allclose(loss.item(), rl.item(), rtol=1e-5)
+    np.testing.assert_allclose(l2.item(), r2.item(), rtol=1e-5)
+    close(tt.grad.cpu().numpy(), T64.grad.numpy(), rtol=1e-4, atol_row=1e-5)
+    close(ww.grad.cpu().numpy(), w64.grad.numpy(), rtol=1e-4, atol_row=1e-5)
+
+
+def test_edge_dropout_and_feat_values(golden):
+    nu, ni, ta = int(golden['n_users']), int(golden['n_items']), golden['train_array']
+    F = O.generate_feat(nu, ni, ta)
+    g = G.Graph(F.row_ptr, F.col.astype(np.int32), F.n_rows, F.n_cols, device=DEV)
+    rs = t(F.row_sum)
+    for tag, alpha in [('a1', 1.0), ('a099sq', float(golden['feat_alpha_a099sq'])),
+                       ('a0', float(golden['feat_alpha_a0']))]:
+        fv = ops.feat_values(g, rs, (alpha - 1.) / 2. - 0.5).cpu().numpy()
+        np.testing.assert_allclose(fv, golden['feat_val_' + tag], rtol=2e-7)
+    rand = golden['igcn_d64_L2_train_rand']
+    fv = golden['feat_val_a1']
+    out = ops.edge_dropout(t(fv), t(rand), 0.3).cpu().numpy()
+    ref = O.dropout_values(fv, rand, 0.3)
+    np.testing.assert_array_equal(out != 0, ref != 0)  # mask bit-exact
+    np.testing.assert_allclose(out, ref, rtol=1e-7)

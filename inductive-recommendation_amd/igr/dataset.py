@@ -107,7 +107,7 @@ class AuxiliaryDataset(BasicDataset):
         self.name = 'AuxiliaryDataset'
         self.n_users = len(user_map)
         self.n_items = len(item_map)
-        self.device = dataset.device
+        self.device = getattr(dataset, 'device', 'cpu')
         self.negative_sample_ratio = 1
         self.length = len(dataset)
         self._pairs = None

@@ -31,7 +31,10 @@ def balanced_ranges(degree, world):
     """Contiguous cut of rows into `world` ranges with ~equal edge counts."""
     cum = np.concatenate([[0], np.cumsum(degree, dtype=np.int64)])
     targets = cum[-1] * np.arange(1, world) / world
-    cuts = np.searchsorted(cum, targets, side='left')
+    cuts = np.clip(np.searchsorted(cum, targets, side='left'), 1, len(cum) - 1)
+    # take the row boundary nearest to each target
+    cuts = np.where(targets - cum[cuts - 1] < cum[cuts] - targets, cuts - 1, cuts)
+    cuts = np.maximum.accumulate(cuts)
     bounds = np.concatenate([[0], cuts, [len(degree)]]).astype(np.int64)
     return [(int(bounds[k]), int(bounds[k + 1])) for k in range(world)]
 
@@ -73,13 +76,15 @@ class BipartiteShard:
         self.item_vals = torch.from_numpy(vals2).to(device)
         self.local_nnz = self.user_block.nnz + self.item_block.nnz
 
-    def layer(self, x_users, x_items, y_users=None, y_items=None, group=None):
-        """One layer: returns (Y[U_k], Y[I]) with Y[I] all-reduced across ranks."""
-        y_items = ops.spmm(self.item_block, x_users, self.item_vals, out=y_items)
+    def layer(self, x_users, x_items, y_users=None, y_items=None, group=None, spmm=None):
+        """One layer: returns (Y[U_k], Y[I]) with Y[I] all-reduced across ranks.
+        `spmm` defaults to the HIP kernel; the CPU gloo tests pass the oracle."""
+        spmm = ops.spmm if spmm is None else spmm
+        y_items = spmm(self.item_block, x_users, self.item_vals, out=y_items)
         work = None
         if self.world > 1:
             work = dist.all_reduce(y_items, op=dist.ReduceOp.SUM, group=group, async_op=True)
-        y_users = ops.spmm(self.user_block, x_items, self.user_vals, out=y_users)
+        y_users = spmm(self.user_block, x_items, self.user_vals, out=y_users)
         if work is not None:
             work.wait()
         return y_users, y_items

@@ -140,7 +140,14 @@ def test_sddmm_and_segment_reduce():
         A = oracle_csr(g, v)
         ref = O.sddmm_dot(A, q.reshape(300, h, d), k.reshape(250, h, d))
         eid = g.host()['edge_id']
-        close(out[eid], ref, rtol=2e-5)
+        # dot products cancel: bound the error by gamma_d * sum_k |q_k k_k| with gamma_d = d * 2^-24
+        # (the fp32 dot-product error bound), against a float64 reference
+        rows = A.rows()
+        qq, kk = q.reshape(300, h, d)[rows].astype(np.float64), k.reshape(250, h, d)[A.col].astype(np.float64)
+        ref64, mag = (qq * kk).sum(-1), np.abs(qq * kk).sum(-1)
+        gamma = d * 2.0 ** -24
+        assert np.all(np.abs(out[eid] - ref64) <= gamma * mag + 1e-30)
+        assert np.all(np.abs(ref - ref64) <= gamma * mag + 1e-30)  # the oracle itself, same bound
     x = rng.standard_normal((g.nnz, 3)).astype(np.float32)
     A = oracle_csr(g, v)
     eid = g.host()['edge_id']
@@ -221,3 +228,16 @@ def test_edge_dropout_and_feat_values(golden):
     ref = O.dropout_values(fv, rand, 0.3)
     np.testing.assert_array_equal(out != 0, ref != 0)  # mask bit-exact
     np.testing.assert_allclose(out, ref, rtol=1e-7)
+
+
+def test_bipartite_shard_world1_matches_oracle():
+    from igr.dist import BipartiteShard
+    U, I, E, d = 3000, 800, 40000, 64
+    rng = np.random.default_rng(12)
+    pairs = np.stack([rng.integers(0, U, E), rng.integers(0, I, E)], 1)
+    sh = BipartiteShard(pairs, U, I, 0, 1, DEV)
+    x = rng.standard_normal((U + I, d)).astype(np.float32)
+    yu, yi = sh.layer(t(x[:U]), t(x[U:]))
+    y64 = O.spmm64(O.norm_adj(U, I, pairs), x)
+    close(yu.cpu().numpy(), y64[:U])
+    close(yi.cpu().numpy(), y64[U:])

@@ -1,0 +1,98 @@
+"""Host-side logic of the model/trainer surface (CPU only)."""
+import numpy as np
+import pytest
+
+from igr import config as C
+from igr import dataset as D
+from igr import model as M
+from igr import ops
+from igr import trainer as T
+from oracle import igr_oracle as O
+
+
+def test_vectorised_calculate_metrics_matches_reference_fixture(golden):
+    topks = golden['eval_topks'].tolist()
+    ptr, items = golden['test_ptr'], golden['test_items']
+    test_data = [items[ptr[u]:ptr[u + 1]].tolist() for u in range(len(ptr) - 1)]
+    res = T.calculate_metrics(test_data, golden['cm_rec_items'], topks)
+    for mk in ['Precision', 'Recall', 'NDCG']:
+        np.testing.assert_allclose([res[mk][k] for k in topks], golden['cm_' + mk], rtol=1e-6)
+
+
+def test_bpr_batch_sampler_semantics():
+    rng = np.random.default_rng(0)
+    pairs = np.stack([rng.integers(0, 50, 600), rng.integers(0, 40, 600)], 1)
+    pairs = pairs[pairs[:, 0] % 7 != 3]  # some users without items
+
+    class DS:
+        n_users, n_items, train_pairs = 50, 40, pairs
+
+        def __len__(self):
+            return len(pairs)
+    s = D.BPRBatchSampler(DS(), 128, seed=1)
+    keys = set(map(tuple, pairs.tolist()))
+    n = 0
+    for u, p, q in s:
+        n += len(u)
+        assert all((a, b) in keys for a, b in zip(u, p))
+        assert not any((a, b) in keys for a, b in zip(u, q))
+        assert np.all(u % 7 != 3)
+    assert n == len(pairs) and len(s) == (len(pairs) + 127) // 128
+
+
+def test_reference_getitem_sampler():
+    ds = D.BasicDataset({'name': 'x'})
+    ds.n_users, ds.n_items = 3, 5
+    ds.train_data = [[0, 1], [], [4]]
+    for _ in range(50):
+        u, p, n = ds[0][0]
+        assert p in ds.train_data[u] and n not in ds.train_data[u]
+
+
+def test_processed_dataset_roundtrip(tmp_path):
+    ds = D.BasicDataset({'name': 'x'})
+    ds.train_data = [[0, 2], [1], [3, 4, 0]]
+    ds.val_data = [[1], [], [2]]
+    ds.test_data = [[3], [0], []]
+    ds.output_dataset(str(tmp_path))
+    p = D.ProcessedDataset({'name': 'ProcessedDataset', 'path': str(tmp_path), 'device': 'cpu'})
+    assert (p.n_users, p.n_items) == (3, 5)
+    assert p.train_array == [[0, 0], [0, 2], [1, 1], [2, 3], [2, 4], [2, 0]]
+    assert p.val_data == ds.val_data and p.test_data == ds.test_data
+
+
+def test_config_rows_are_on_path():
+    for rows in [C.get_ml_config('cuda'), C.get_gowalla_config('cuda')]:
+        names = {m['name'] for _, m, _ in rows}
+        assert names <= {'LightGCN', 'IGCN', 'IMF', 'NGCF'}
+        igcn = next((m, t) for _, m, t in rows if m['name'] == 'IGCN')
+        assert igcn[0]['dropout'] == 0.3 and igcn[1]['aux_reg'] == 0.01 and igcn[1]['batch_size'] == 2048
+
+
+def test_models_need_the_hip_device(golden):
+    class DS:
+        n_users, n_items = int(golden['n_users']), int(golden['n_items'])
+        train_pairs = golden['train_array']
+    with pytest.raises(ops.IgrError, match='no CPU fallback'):
+        M.IGCN({'name': 'IGCN', 'embedding_size': 16, 'n_layers': 1, 'device': 'cpu', 'dropout': 0.3,
+                'feature_ratio': 1., 'dataset': DS()})
+
+
+def test_synthetic_pairs_reproducible():
+    a = D.synthetic_pairs(1000, 100, 5000, seed=3)
+    b = D.synthetic_pairs(1000, 100, 5000, seed=3)
+    np.testing.assert_array_equal(a, b)
+    assert a[:, 0].max() < 1000 and a[:, 1].max() < 100
+    z = D.synthetic_pairs(1000, 100, 20000, seed=1, item_dist='zipf')
+    c = np.bincount(z[:, 1], minlength=100)
+    assert c[0] > 5 * c[50]
+
+
+def test_rank_nodes_degree(golden):
+    class DS:
+        n_users, n_items = int(golden['n_users']), int(golden['n_items'])
+        train_pairs = golden['train_array']
+    ru, ri = M.graph_rank_nodes(DS(), 'degree')
+    A = O.generate_daj_mat(DS.n_users, DS.n_items, DS.train_pairs)
+    deg = O.row_sums(A)
+    assert np.all(np.diff(deg[ru]) <= 0) and np.all(np.diff(deg[DS.n_users + ri]) <= 0)

@@ -85,6 +85,7 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='CPU baseline budget (0 = skip)')
     ap.add_argument('--cpu-sample-edges', type=int, default=20_000_000)
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'))
+    ap.add_argument('--item-tiles', default='auto', help="source tiles of the item-side SpMM ('auto' or an int)")
     args = ap.parse_args()
 
     rank = int(os.environ.get('RANK', 0))
@@ -105,7 +106,7 @@ def main():
     log(f'rank {rank}/{world}: drawing {E} interactions (U={U}, I={I}, {args.item_dist}, seed {args.seed})')
     pairs = synthetic_pairs(U, I, E, args.seed, args.item_dist)
     log(f'building shard (C++ CSR build) ... {time.time() - t0:.1f}s')
-    shard = BipartiteShard(pairs, U, I, rank, world, dev)
+    shard = BipartiteShard(pairs, U, I, rank, world, dev, d=d, item_tiles=args.item_tiles)
     del pairs
     nu = shard.u1 - shard.u0
     log(f'shard users [{shard.u0}, {shard.u1}) local nnz {shard.local_nnz} '
@@ -118,25 +119,22 @@ def main():
     y_users = torch.empty(nu, d, device=dev)
     y_items = torch.empty(I, d, device=dev)
     stream = torch.cuda.current_stream()
-    blocks = [(shard.item_block, shard.item_vals, x_users, y_items), (shard.user_block, shard.user_vals, x_items, y_users)]
-    launch_bytes = [spmm_bytes(b.nnz, b.n_rows, d) for b, _, _, _ in blocks]
+    launches = shard.launches()
+    launch_bytes = [spmm_bytes(nnz, n_rows, d) for _, _, _, n_rows, nnz in launches]
+    log('launches per step: ' + ', '.join(f'{n}(rows={r}, nnz={z})' for n, _, _, r, z in launches))
 
     def step(events=None):
-        for k, (blk, vals, x, y) in enumerate(blocks):
-            if events is not None:
-                events[k][0].record(stream)
-            ops.spmm(blk, x, vals, out=y)
-            if events is not None:
-                events[k][1].record(stream)
-            if k == 0 and world > 1:
-                work = dist.all_reduce(y_items, op=dist.ReduceOp.SUM, async_op=True)
-        if world > 1:
-            work.wait()
+        hook = None
+        if events is not None:
+            def hook(i, ph):
+                events[i][0 if ph == 'start' else 1].record(stream)
+        shard.layer(x_users, x_items, y_users, y_items, hook=hook)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ev = [[[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(2)] for _ in range(args.steps)]
+    nl = len(launches)
+    ev = [[[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(nl)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -147,7 +145,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    kern_ms = np.array([[ev[s][k][0].elapsed_time(ev[s][k][1]) for k in range(2)] for s in range(args.steps)])
+    kern_ms = np.array([[ev[s][k][0].elapsed_time(ev[s][k][1]) for k in range(nl)] for s in range(args.steps)])
 
     stats = torch.tensor([elapsed, float(shard.local_nnz)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -166,10 +164,11 @@ def main():
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        key = f'd{d}_U{U}_I{I}_E{E}_w{world}'
+        key = f'd{d}_U{U}_I{I}_E{E}_w{world}_T{shard.item_tiles}'
         traffic = tj.get(key, {}).get('hbm_bytes_per_launch')
-    log(f'elapsed {elapsed:.4f}s for {args.steps} steps; kernel avg {avg_kernel_s * 1e3:.3f} ms '
-        f'(user {kern_ms[:, 1].mean():.3f} ms, item {kern_ms[:, 0].mean():.3f} ms); {achieved:.0f} GB/s algorithmic')
+    log(f'elapsed {elapsed:.4f}s for {args.steps} steps; SpMM launch avg {avg_kernel_s * 1e3:.3f} ms; per launch ' +
+        ', '.join(f'{n} {kern_ms[:, k].mean():.3f} ms' for k, (n, *_r) in enumerate(launches)) +
+        f'; {achieved:.0f} GB/s algorithmic')
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -185,10 +184,11 @@ def main():
             'config': {'workload': f'synthetic bipartite {U} users x {I} items, {E} {args.item_dist} draws, '
                                    f'd={d}: one SpMM layer Y = D^-1/2 A D^-1/2 X over all {total_nnz} edges',
                        'n_users': U, 'n_items': I, 'n_draws': E, 'nnz': total_nnz, 'd': d,
-                       'parallelism': f'user-range shards x{world}, item block replicated, RCCL all-reduce'},
+                       'parallelism': f'user-range shards x{world}, item block replicated, RCCL all-reduce',
+                       'item_source_tiles': shard.item_tiles, 'launches_per_step': nl},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic,
-                         'kernel': 'igr::spmm_main<64,true,false>',
+                         'kernel': f'igr::spmm_main<{d},true,false>',
                          'avg_launch_ms': avg_kernel_s * 1e3, 'algorithmic_bytes_per_launch': avg_bytes},
             'cpu_baseline': cpu,
         }

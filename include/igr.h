@@ -123,12 +123,14 @@ int igr_sym_norm_values(int64_t n_rows, const int64_t *row_ptr, const int32_t *c
 
 /* Row schedule.  igr_plan_size returns the array sizes, igr_plan_fill fills
  * host arrays that the caller copies to the device and references from
- * igr_csr. */
+ * igr_csr.  Short rows are ordered by degree, descending, inside windows of
+ * `window` consecutive rows (0 = one global window); long rows are chunked and
+ * ordered heaviest first. */
 int igr_plan_size(int64_t n_rows, const int64_t *row_ptr, int64_t split_threshold,
                   int64_t chunk_edges, int64_t *n_order, int64_t *n_split, int64_t *n_chunks);
 int igr_plan_fill(int64_t n_rows, const int64_t *row_ptr, int64_t split_threshold,
-                  int64_t chunk_edges, int32_t *order, int32_t *split_row, int64_t *split_ptr,
-                  int32_t *chunk_row, int64_t *chunk_beg);
+                  int64_t chunk_edges, int64_t window, int32_t *order, int32_t *split_row,
+                  int64_t *split_ptr, int32_t *chunk_row, int64_t *chunk_beg);
 
 /* ------------------------------------------------------- device kernels */
 

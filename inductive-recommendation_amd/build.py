@@ -18,7 +18,7 @@ SOURCES = ['spmm.hip', 'edge_ops.hip', 'bpr.hip', 'gemm.hip', 'graph_host.cpp', 
 ARCH = os.environ.get('IGR_OFFLOAD_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 CFLAGS = ['-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-I', INCLUDE, '-I', CSRC,
-          '-Wall', '-Wno-unused-function']
+          '-Wall', '-Wno-unused-function'] + os.environ.get('IGR_EXTRA_CFLAGS', '').split()
 
 
 def _newer(target, deps):
@@ -28,7 +28,10 @@ def _newer(target, deps):
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
-def build(verbose=False, jobs=8):
+def build(verbose=False, jobs=8, lib=None, obj=None):
+    """Compile and link; `lib`/`obj` override the output paths (tuning variants)."""
+    global LIB, OBJ
+    LIB, OBJ = lib or LIB, obj or OBJ
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     headers = [os.path.join(CSRC, 'common.h'), os.path.join(INCLUDE, 'igr.h')]

@@ -238,25 +238,37 @@ extern "C" int igr_plan_size(int64_t n_rows, const int64_t *row_ptr, int64_t spl
 }
 
 extern "C" int igr_plan_fill(int64_t n_rows, const int64_t *row_ptr, int64_t split_threshold,
-                             int64_t chunk_edges, int32_t *order, int32_t *split_row,
+                             int64_t chunk_edges, int64_t window, int32_t *order, int32_t *split_row,
                              int64_t *split_ptr, int32_t *chunk_row, int64_t *chunk_beg) {
     return guarded("igr_plan_fill", [&]() -> int {
-        if (n_rows < 0 || !row_ptr || split_threshold < 1 || chunk_edges < 64 || chunk_edges % 64)
+        if (n_rows < 0 || !row_ptr || split_threshold < 1 || chunk_edges < 64 || chunk_edges % 64 || window < 0)
             return arg_error("igr_plan_fill", "bad args");
         const int64_t thr = split_threshold;
-        // counting sort of short rows by degree, descending; ties by row id
-        std::vector<int64_t> bucket(thr + 2, 0);
+        const int64_t win = window > 0 ? window : std::max<int64_t>(n_rows, 1);
+        // Short rows: counting sort by degree, descending, inside windows of `win`
+        // consecutive rows (ties by row id).  Windows keep the row_ptr reads and
+        // output writes of one stretch of the launch inside an L2-sized range;
+        // window = 0 sorts globally (heaviest first over the whole graph).
+        std::vector<int64_t> bucket(thr + 2);
         std::vector<int32_t> longs;
-        for (int64_t r = 0; r < n_rows; ++r) {
-            const int64_t deg = row_ptr[r + 1] - row_ptr[r];
-            if (deg > thr) longs.push_back((int32_t)r);
-            else bucket[thr - deg + 1]++;
+        int64_t o = 0;
+        for (int64_t w0 = 0; w0 < n_rows; w0 += win) {
+            const int64_t w1 = std::min(n_rows, w0 + win);
+            std::fill(bucket.begin(), bucket.end(), 0);
+            for (int64_t r = w0; r < w1; ++r) {
+                const int64_t deg = row_ptr[r + 1] - row_ptr[r];
+                if (deg > thr) longs.push_back((int32_t)r);
+                else bucket[thr - deg + 1]++;
+            }
+            bucket[0] = o;
+            for (int64_t i = 0; i <= thr; ++i) bucket[i + 1] += bucket[i];
+            for (int64_t r = w0; r < w1; ++r) {
+                const int64_t deg = row_ptr[r + 1] - row_ptr[r];
+                if (deg <= thr) order[bucket[thr - deg]++] = (int32_t)r;
+            }
+            o = bucket[thr];
         }
-        for (int64_t i = 0; i <= thr; ++i) bucket[i + 1] += bucket[i];
-        for (int64_t r = 0; r < n_rows; ++r) {
-            const int64_t deg = row_ptr[r + 1] - row_ptr[r];
-            if (deg <= thr) order[bucket[thr - deg]++] = (int32_t)r;
-        }
+        // long rows: globally heaviest first, dispatched before every short row
         std::stable_sort(longs.begin(), longs.end(), [&](int32_t a, int32_t b) {
             return row_ptr[a + 1] - row_ptr[a] > row_ptr[b + 1] - row_ptr[b];
         });

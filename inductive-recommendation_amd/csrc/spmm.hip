@@ -80,49 +80,54 @@ __device__ __forceinline__ float edge_weight(const float *__restrict__ val,
     }
 }
 
-constexpr int kUnroll = 8;
+#ifndef IGR_SPMM_UNROLL
+#define IGR_SPMM_UNROLL 16
+#endif
+#ifndef IGR_SPMM_MIN_WAVES
+#define IGR_SPMM_MIN_WAVES 1
+#endif
 
 // Accumulate the first n edges of a block whose (col, val) pairs live in lanes
 // gbase .. gbase+n-1 of the caller's own lane group (shuffles never leave the
-// group, so divergence between groups is harmless).  All loads of a step of
-// kUnroll are issued before their FMAs.
+// group, so divergence between groups is harmless).  Steps of U edges issue
+// all U row gathers before their FMAs; the last partial step masks its
+// out-of-range slots (no load is issued for them).
+template <int U>
 __device__ __forceinline__ float4 gather_block(float4 acc, int cl, float vl, int gbase, int n,
                                                const float *__restrict__ xs, int64_t ldx) {
     int k = 0;
-    for (; k + kUnroll <= n; k += kUnroll) {
-        float4 xv[kUnroll];
-        float wv[kUnroll];
+    for (; k + U <= n; k += U) {
+        float4 xv[U];
+        float wv[U];
 #pragma unroll
-        for (int j = 0; j < kUnroll; ++j) {
-            const int c = shfl_i(cl, gbase + (k + j));
-            wv[j] = shfl_f(vl, gbase + (k + j));
+        for (int j = 0; j < U; ++j) {
+            const int c = shfl_i(cl, gbase + k + j);
+            wv[j] = shfl_f(vl, gbase + k + j);
             xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
         }
 #pragma unroll
-        for (int j = 0; j < kUnroll; ++j) acc = f4_fma(wv[j], xv[j], acc);
+        for (int j = 0; j < U; ++j) acc = f4_fma(wv[j], xv[j], acc);
     }
     if (k < n) {
-        // predicated remainder: out-of-range slots re-read the last valid row
-        // (a cache hit) and are masked out of the sum.
-        float4 xv[kUnroll];
-        float wv[kUnroll];
-        const int last = n - 1;
+        float4 xv[U];
+        float wv[U];
 #pragma unroll
-        for (int j = 0; j < kUnroll; ++j) {
-            const int kk = min(k + j, last);
-            const int c = shfl_i(cl, gbase + kk);
-            wv[j] = shfl_f(vl, gbase + kk);
-            xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
+        for (int j = 0; j < U; ++j) {
+            if (k + j < n) {
+                const int c = shfl_i(cl, gbase + k + j);
+                wv[j] = shfl_f(vl, gbase + k + j);
+                xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
+            }
         }
 #pragma unroll
-        for (int j = 0; j < kUnroll; ++j)
+        for (int j = 0; j < U; ++j)
             if (k + j < n) acc = f4_fma(wv[j], xv[j], acc);
     }
     return acc;
 }
 
 template <int D, bool VAL, bool EID>
-__global__ __launch_bounds__(256) void spmm_main(
+__global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
     const int64_t *__restrict__ eid, const float *__restrict__ val, const float *__restrict__ x,
     int64_t ldx, const int32_t *__restrict__ order, int64_t n_order,
@@ -130,6 +135,7 @@ __global__ __launch_bounds__(256) void spmm_main(
     int64_t chunk_edges, float *__restrict__ ws, int64_t chunk_blocks, Epi epi) {
     constexpr int LPR = D / 4;   // lanes per feature row
     constexpr int G = 64 / LPR;  // groups per wave
+    constexpr int U = IGR_SPMM_UNROLL < LPR ? IGR_SPMM_UNROLL : LPR;  // gathers in flight per group
     const int lane = threadIdx.x & 63;
     const int grp = lane / LPR;
     const int sub = lane - grp * LPR;
@@ -164,7 +170,7 @@ __global__ __launch_bounds__(256) void spmm_main(
             // group grp takes edges [grp*LPR, grp*LPR + LPR) of this 64-edge block,
             // i.e. exactly the (col, val) pairs its own lanes loaded
             const int m = min(max(n - grp * LPR, 0), LPR);
-            acc = gather_block(acc, cl, vl, grp * LPR, m, xs, ldx);
+            acc = gather_block<U>(acc, cl, vl, grp * LPR, m, xs, ldx);
             base = nb;
             n = nn;
             cl = cl2;
@@ -206,7 +212,7 @@ __global__ __launch_bounds__(256) void spmm_main(
             cl2 = ld_stream(col + nb + sub);
             vl2 = edge_weight<VAL, EID>(val, eid, nb + sub);
         }
-        acc = gather_block(acc, cl, vl, gbase, n, xs, ldx);
+        acc = gather_block<U>(acc, cl, vl, gbase, n, xs, ldx);
         base = nb;
         n = nn;
         cl = cl2;

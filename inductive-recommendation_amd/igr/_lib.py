@@ -50,7 +50,7 @@ SIGNATURES = {
     'igr_csr_row_sums': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp]),
     'igr_sym_norm_values': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'igr_plan_size': (ctypes.c_int, [c_i64, c_vp, c_i64, c_i64, _P(c_i64), _P(c_i64), _P(c_i64)]),
-    'igr_plan_fill': (ctypes.c_int, [c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'igr_plan_fill': (ctypes.c_int, [c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'igr_spmm_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, _P(IgrEpilogue), c_vp, c_vp]),
     'igr_sddmm_dot_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     'igr_segment_reduce_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i32, c_vp, c_vp]),

@@ -19,6 +19,7 @@ from . import _lib as L
 
 DEFAULT_SPLIT_THRESHOLD = 512
 DEFAULT_CHUNK_EDGES = 512
+DEFAULT_WINDOW = 65536  # degree-sort window (rows); 0 = global
 
 
 def _ptr(a):
@@ -87,7 +88,7 @@ def sym_norm_values(row_ptr, col_idx, val, dinv, dinv_col=None):
     return out
 
 
-def plan(row_ptr, split_threshold=DEFAULT_SPLIT_THRESHOLD, chunk_edges=DEFAULT_CHUNK_EDGES):
+def plan(row_ptr, split_threshold=DEFAULT_SPLIT_THRESHOLD, chunk_edges=DEFAULT_CHUNK_EDGES, window=None):
     """Degree-binned row schedule (see include/igr.h igr_plan_fill)."""
     row_ptr = _np(row_ptr, np.int64)
     n_rows = len(row_ptr) - 1
@@ -99,7 +100,8 @@ def plan(row_ptr, split_threshold=DEFAULT_SPLIT_THRESHOLD, chunk_edges=DEFAULT_C
     split_ptr = np.empty(ns.value + 1, np.int64)
     chunk_row = np.empty(max(nc.value, 1), np.int32)
     chunk_beg = np.empty(max(nc.value, 1), np.int64)
-    L.call('igr_plan_fill', n_rows, _ptr(row_ptr), split_threshold, chunk_edges, _ptr(order),
+    window = DEFAULT_WINDOW if window is None else window
+    L.call('igr_plan_fill', n_rows, _ptr(row_ptr), split_threshold, chunk_edges, window, _ptr(order),
            _ptr(split_row), _ptr(split_ptr), _ptr(chunk_row), _ptr(chunk_beg))
     return dict(order=order[:no.value], split_row=split_row[:ns.value], split_ptr=split_ptr,
                 chunk_row=chunk_row[:nc.value], chunk_beg=chunk_beg[:nc.value], chunk_edges=chunk_edges)
@@ -115,7 +117,7 @@ class Graph:
     unsorted edge list)."""
 
     def __init__(self, row_ptr, col_idx, n_rows, n_cols, device='cuda', edge_id=None, symmetric=False,
-                 split_threshold=DEFAULT_SPLIT_THRESHOLD, chunk_edges=DEFAULT_CHUNK_EDGES):
+                 split_threshold=DEFAULT_SPLIT_THRESHOLD, chunk_edges=DEFAULT_CHUNK_EDGES, window=None):
         row_ptr = _np(row_ptr, np.int64)
         col_idx = _np(col_idx, np.int32)
         self.n_rows, self.n_cols = int(n_rows), int(n_cols)
@@ -130,7 +132,8 @@ class Graph:
         self.symmetric = symmetric
         self.split_threshold, self.chunk_edges = split_threshold, chunk_edges
         self._host = dict(row_ptr=row_ptr, col_idx=col_idx, edge_id=edge_id)
-        p = plan(row_ptr, split_threshold, chunk_edges)
+        p = plan(row_ptr, split_threshold, chunk_edges, window)
+        self.window = window
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)  # noqa: E731
         self.row_ptr = t(row_ptr)
         self.col_idx = t(col_idx)
@@ -204,3 +207,36 @@ class Graph:
     def __repr__(self):
         return (f'Graph(n_rows={self.n_rows}, n_cols={self.n_cols}, nnz={self.nnz}, split_rows={self.n_split}, '
                 f'chunks={self.n_chunks}, device={self.device})')
+
+
+class TiledGraph:
+    """A graph cut into source-column tiles: A = [A_0 | A_1 | ... ] by column range.
+
+    y = sum_t A_t x[cols_t] is computed tile by tile, accumulating in place,
+    so each pass gathers from a table slice small enough to stay resident in
+    the Infinity Cache instead of streaming the whole source table from HBM.
+    Pays off when the gathered table is much larger than the output
+    (the item side of a user x item graph).  `perm` maps each tile's edge
+    positions to positions of the parent CSR (to slice edge values)."""
+
+    def __init__(self, parent_host, n_rows, n_cols, bounds, device, **kw):
+        rp, ci = parent_host['row_ptr'], parent_host['col_idx']
+        nnz = int(rp[-1])
+        rows = np.repeat(np.arange(n_rows, dtype=np.int64), np.diff(rp))
+        tile = np.searchsorted(np.asarray(bounds[1:-1], np.int64), ci, side='right').astype(np.int16)
+        order = np.argsort(tile, kind='stable')  # edges grouped by tile, CSR order within a tile
+        counts = np.bincount(tile, minlength=len(bounds) - 1)
+        self.tiles, self.perms, self.bounds = [], [], list(bounds)
+        start = 0
+        for t in range(len(bounds) - 1):
+            sel = order[start:start + counts[t]]
+            start += counts[t]
+            trp = np.concatenate([[0], np.cumsum(np.bincount(rows[sel], minlength=n_rows))]).astype(np.int64)
+            tci = (ci[sel] - bounds[t]).astype(np.int32)
+            self.tiles.append(Graph(trp, tci, n_rows, bounds[t + 1] - bounds[t], device=device, **kw))
+            self.perms.append(torch.from_numpy(sel).to(device))
+        self.n_rows, self.n_cols, self.nnz = n_rows, n_cols, nnz
+
+    def tile_values(self, vals):
+        """Per-tile contiguous value arrays (gathered once; values by parent CSR position)."""
+        return [vals[p].contiguous() for p in self.perms]

@@ -472,3 +472,16 @@ def gsddmm(g, op, lhs_data, rhs_data, h=1):
 
 def sqrt_scale(d):
     return float(np.float32(math.sqrt(d)))
+
+
+def spmm_tiled(tg, x, tile_vals, out=None):
+    """y = A x over a TiledGraph: first tile writes, later tiles accumulate in place."""
+    _dev(x)
+    x, ldx = _rows(x)
+    d = x.shape[1]
+    if out is None:
+        out = torch.empty(tg.n_rows, d, dtype=torch.float32, device=x.device)
+    for t, (g, v) in enumerate(zip(tg.tiles, tile_vals)):
+        xs = x[tg.bounds[t]:tg.bounds[t + 1]]
+        spmm(g, xs, v, out=out, epi=None if t == 0 else epilogue(beta=1.0, add=out))
+    return out

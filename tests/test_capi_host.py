@@ -78,7 +78,7 @@ def test_plan_covers_rows_heaviest_first():
     rng = np.random.default_rng(3)
     deg = np.concatenate([rng.integers(0, 40, 500), [0, 0, 2000, 700, 5000, 513, 512]])
     rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
-    p = G.plan(rp, split_threshold=512, chunk_edges=256)
+    p = G.plan(rp, split_threshold=512, chunk_edges=256, window=0)
     order, sr, sp, cr, cb = p['order'], p['split_row'], p['split_ptr'], p['chunk_row'], p['chunk_beg']
     assert sorted(np.concatenate([order, sr]).tolist()) == list(range(len(deg)))
     assert np.all(deg[order] <= 512) and np.all(deg[sr] > 512)
@@ -87,6 +87,15 @@ def test_plan_covers_rows_heaviest_first():
         chunks = list(range(sp[s], sp[s + 1]))
         assert all(cr[c] == r for c in chunks)
         np.testing.assert_array_equal(cb[chunks], np.arange(rp[r], rp[r + 1], 256))
+    # windowed: each window of 100 rows is a degree-descending run, windows in row order
+    pw = G.plan(rp, split_threshold=512, chunk_edges=256, window=100)
+    ow = pw['order']
+    assert sorted(ow.tolist()) == sorted(order.tolist())
+    win = ow // 100
+    assert np.all(np.diff(win) >= 0)
+    for w in np.unique(win):
+        assert np.all(np.diff(deg[ow[win == w]]) <= 0)
+    np.testing.assert_array_equal(pw['split_row'], sr)
 
 
 def test_norm_adj_host_build_bit_exact(golden):

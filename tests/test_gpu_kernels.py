@@ -241,3 +241,27 @@ def test_bipartite_shard_world1_matches_oracle():
     y64 = O.spmm64(O.norm_adj(U, I, pairs), x)
     close(yu.cpu().numpy(), y64[:U])
     close(yi.cpu().numpy(), y64[U:])
+
+
+def test_tiled_spmm_matches_oracle():
+    g, v = rand_graph(3000, 20000, 120000, seed=29)
+    x = np.random.default_rng(13).standard_normal((20000, 64)).astype(np.float32)
+    tg = G.TiledGraph(g.host(), g.n_rows, g.n_cols, [0, 5000, 12000, 20000], DEV)
+    y = ops.spmm_tiled(tg, t(x), tg.tile_values(t(v))).cpu().numpy()
+    close(y, O.spmm64(oracle_csr(g, v), x), atol_row=2e-6)
+
+
+def test_bipartite_shard_tiled_items():
+    from igr.dist import BipartiteShard
+    U, I, E, d = 20000, 500, 100000, 64
+    rng = np.random.default_rng(14)
+    pairs = np.stack([rng.integers(0, U, E), rng.integers(0, I, E)], 1)
+    sh = BipartiteShard(pairs, U, I, 0, 1, DEV, item_tiles=3)
+    assert sh.item_tiled is not None and len(sh.launches()) == 4
+    x = rng.standard_normal((U + I, d)).astype(np.float32)
+    calls = []
+    yu, yi = sh.layer(t(x[:U]), t(x[U:]), hook=lambda i, ph: calls.append((i, ph)))
+    assert calls == [(i, ph) for i in range(4) for ph in ('start', 'end')]
+    y64 = O.spmm64(O.norm_adj(U, I, pairs), x)
+    close(yu.cpu().numpy(), y64[:U])
+    close(yi.cpu().numpy(), y64[U:], atol_row=2e-6)

@@ -86,16 +86,23 @@ def main():
     ap.add_argument('--cpu-sample-edges', type=int, default=20_000_000)
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'))
     ap.add_argument('--item-tiles', default='auto', help="source tiles of the item-side SpMM ('auto' or an int)")
+    ap.add_argument('--dist-backend', default='nccl', help="'nccl' (= RCCL on ROCm); 'gloo' only for rehearsals")
+    ap.add_argument('--one-device', action='store_true',
+                    help='map every rank to cuda:0 (multi-rank rehearsal on a one-GPU box, with --dist-backend gloo)')
     args = ap.parse_args()
 
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local_rank = int(os.environ.get('LOCAL_RANK', 0))
     assert world == args.gpus, f'--gpus {args.gpus} but WORLD_SIZE={world}'
-    torch.cuda.set_device(local_rank)
-    dev = torch.device('cuda', local_rank)
+    dev_index = 0 if args.one_device else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device('cuda', dev_index)
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)  # RCCL over xGMI
+        if args.dist_backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)  # RCCL over xGMI
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from igr import ops
     from igr.dataset import synthetic_pairs

@@ -209,6 +209,25 @@ int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int64_t lda, i
                  const float *b, int64_t ldb, int32_t trans_b, const float *bias, float *c,
                  int64_t ldc, void *stream);
 
+/* ------------------------------------------------------- training step */
+
+/* Device-side BPR sampler (dataset.py:119-131 semantics):
+ * for each b < batch: users[b] = active[uniform], pos[b] = uniform item of that
+ * user's sorted training list items[row_ptr[u] .. row_ptr[u+1]), neg[b] =
+ * uniform item not in that list (rejection, at most max_rounds redraws).
+ * Counter-based RNG: the draw is a pure function of (seed, offset, b), so a
+ * step is reproducible and needs no RNG state. */
+int igr_bpr_sample(int64_t batch, int64_t n_active, const int32_t *active, const int64_t *row_ptr,
+                   const int32_t *items, int64_t n_items, uint64_t seed, uint64_t offset,
+                   int32_t max_rounds, int64_t *users, int64_t *pos, int64_t *neg, void *stream);
+
+/* Fused Adam step (torch.optim.Adam semantics, amsgrad off; trainer.py:44-46,
+ * 555): one pass over p, g, m, v.  `step` is the 1-based
+ * step count after increment (bias corrections). */
+int igr_adam_f32(int64_t n, float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
+                 double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
+                 void *stream);
+
 #ifdef __cplusplus
 }
 #endif

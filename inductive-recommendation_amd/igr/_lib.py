@@ -64,6 +64,10 @@ SIGNATURES = {
                                            c_vp, c_vp, c_f32, c_f32, c_vp, c_i64, c_vp, c_vp]),
     'igr_gemm_f32': (ctypes.c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp, c_vp,
                                     c_i64, c_vp]),
+    'igr_bpr_sample': (ctypes.c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, ctypes.c_uint64, ctypes.c_uint64,
+                                      c_i32, c_vp, c_vp, c_vp, c_vp]),
+    'igr_adam_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,
+                                    ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i64, c_vp]),
 }
 
 _lib = None

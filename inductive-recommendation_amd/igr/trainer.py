@@ -9,6 +9,11 @@ trainer config runs the reference's exact op sequence on bpr_forward.
 Evaluation computes the representation once per eval instead of once per
 512-user batch (the reference's predict re-propagates, model.py:123); in
 eval mode both are the same function of the weights.
+
+Trainer config extensions (all optional): 'sampler': 'device' (default, HIP
+sampler, igr.sampler) or 'host' (vectorised numpy); 'fused' (default True);
+'seed'.  The epoch loss is accumulated on the device and read once per epoch
+(the reference syncs with loss.item() every step, trainer.py:556).
 """
 import os
 import sys
@@ -17,10 +22,12 @@ import time
 import numpy as np
 import torch
 import torch.nn.functional as F
-from torch.optim import SGD, Adam  # noqa: F401  (resolved by name, trainer.py:44-46)
+from torch.optim import SGD  # noqa: F401  (resolved by name, trainer.py:44-46)
+from torch.optim import Adam as TorchAdam  # noqa: F401
 
 from .dataset import AuxiliaryDataset, BPRBatchSampler
-from .utils import AverageMeter
+from .optim import Adam  # noqa: F401  fused HIP Adam, resolved by name 'Adam'
+from .sampler import DeviceBPRSampler
 
 
 def get_trainer(config, dataset, model):
@@ -187,12 +194,22 @@ class BasicTrainer:
         return results, metrics
 
 
+def make_sampler(trainer_config, dataset, seed):
+    if trainer_config.get('sampler', 'device') == 'device' and torch.device(trainer_config['device']).type == 'cuda':
+        return DeviceBPRSampler(dataset, trainer_config['batch_size'], trainer_config['device'], seed or 0)
+    return BPRBatchSampler(dataset, trainer_config['batch_size'], seed)
+
+
+def _dev_batch(batch, device):
+    return tuple(b if isinstance(b, torch.Tensor) else torch.from_numpy(b).to(device) for b in batch)
+
+
 class BPRTrainer(BasicTrainer):
     """trainer.py:403-429."""
 
     def __init__(self, trainer_config):
         super().__init__(trainer_config)
-        self.sampler = BPRBatchSampler(self.dataset, trainer_config['batch_size'], trainer_config.get('seed'))
+        self.sampler = make_sampler(trainer_config, self.dataset, trainer_config.get('seed'))
         self.initialize_optimizer()
         self.l2_reg = trainer_config['l2_reg']
         self.fused = trainer_config.get('fused', True)
@@ -213,12 +230,13 @@ class BPRTrainer(BasicTrainer):
         return loss
 
     def train_one_epoch(self):
-        losses = AverageMeter()
-        for u, p, n in self.sampler:
-            t = lambda a: torch.from_numpy(a).to(self.device)  # noqa: E731
-            loss = self.step(t(u), t(p), t(n))
-            losses.update(loss.item(), len(u))
-        return losses.avg
+        tot, cnt = None, 0
+        for batch in self.sampler:
+            u, p, n = _dev_batch(batch, self.device)
+            loss = self.step(u, p, n).detach() * len(u)
+            tot = loss if tot is None else tot + loss
+            cnt += len(u)
+        return float(tot) / cnt
 
 
 class IGCNTrainer(BasicTrainer):
@@ -226,11 +244,11 @@ class IGCNTrainer(BasicTrainer):
 
     def __init__(self, trainer_config):
         super().__init__(trainer_config)
-        bs = trainer_config['batch_size']
         seed = trainer_config.get('seed')
-        self.sampler = BPRBatchSampler(self.dataset, bs, seed)
-        self.aux_sampler = BPRBatchSampler(AuxiliaryDataset(self.dataset, self.model.user_map, self.model.item_map),
-                                           bs, None if seed is None else seed + 1)
+        self.sampler = make_sampler(trainer_config, self.dataset, seed)
+        self.aux_sampler = make_sampler(trainer_config,
+                                        AuxiliaryDataset(self.dataset, self.model.user_map, self.model.item_map),
+                                        None if seed is None else seed + 1)
         self.initialize_optimizer()
         self.l2_reg = trainer_config['l2_reg']
         self.aux_reg = trainer_config['aux_reg']
@@ -256,10 +274,12 @@ class IGCNTrainer(BasicTrainer):
         return loss
 
     def train_one_epoch(self):
-        losses = AverageMeter()
-        t = lambda a: torch.from_numpy(a).to(self.device)  # noqa: E731
-        for (u, p, n), (au, ap, an) in zip(self.sampler, self.aux_sampler):
-            loss = self.step(t(u), t(p), t(n), t(au), t(ap), t(an))
-            losses.update(loss.item(), len(au))
+        tot, cnt = None, 0
+        for main, aux in zip(self.sampler, self.aux_sampler):
+            u, p, n = _dev_batch(main, self.device)
+            au, ap, an = _dev_batch(aux, self.device)
+            loss = self.step(u, p, n, au, ap, an).detach() * len(au)
+            tot = loss if tot is None else tot + loss
+            cnt += len(au)
         self.model.feat_mat_anneal()
-        return losses.avg
+        return float(tot) / cnt

@@ -190,7 +190,7 @@ def main():
         fx['norm_idx'] = idx
         fx['norm_val'] = val
 
-        # --- LightGCN get_rep (model.py:100-110) at (d, L) in {(32,1), (64,2)}
+        # --- LightGCN get_rep (model.py:100-110) at (d, L) in {(32,1), (64,2)}, + gradient
         for d, L in [(32, 1), (64, 2)]:
             torch.manual_seed(100 + d + L)
             m = ref_model.LightGCN(model_cfg('LightGCN', ds, d, L))
@@ -199,6 +199,30 @@ def main():
                 rep = m.get_rep()
             fx[f'lgcn_d{d}_L{L}_emb'] = m.embedding.weight.detach().numpy().copy()
             fx[f'lgcn_d{d}_L{L}_rep'] = rep.numpy().copy()
+            R = torch.randn(rep.shape, generator=torch.Generator().manual_seed(8))
+            (m.get_rep() * R).sum().backward()
+            fx[f'lgcn_d{d}_L{L}_R'] = R.numpy()
+            fx[f'lgcn_d{d}_L{L}_grad'] = m.embedding.weight.grad.numpy().copy()
+
+        # --- NGCF (model.py:3986-4055), eval mode: SpMM + 2 Linear + LeakyReLU + normalize, concat
+        torch.manual_seed(500)
+        m = ref_model.NGCF({'name': 'NGCF', 'embedding_size': 32, 'layer_sizes': [32, 32], 'device': 'cpu',
+                            'dropout': 0.1, 'dataset': ds})
+        m.eval()
+        ni_, nv_ = sp_np(m.norm_adj)
+        fx['ngcf_norm_idx'], fx['ngcf_norm_val'] = ni_, nv_
+        fx['ngcf_emb'] = m.embedding.weight.detach().numpy().copy()
+        for li in range(2):
+            for nm, lay in [('gc', m.gc_layers[li]), ('bi', m.bi_layers[li])]:
+                fx[f'ngcf_{nm}{li}_w'] = lay.weight.detach().numpy().copy()
+                fx[f'ngcf_{nm}{li}_b'] = lay.bias.detach().numpy().copy()
+        rep = m.get_rep()
+        fx['ngcf_rep'] = rep.detach().numpy().copy()
+        R = torch.randn(rep.shape, generator=torch.Generator().manual_seed(9))
+        (rep * R).sum().backward()
+        fx['ngcf_R'] = R.numpy()
+        fx['ngcf_grad'] = m.embedding.weight.grad.numpy().copy()
+        fx['ngcf_gc0_wgrad'] = m.gc_layers[0].weight.grad.numpy().copy()
 
         # --- IGCN: feat_mat (model.py:4139-4175), alpha anneal (4127-4134), get_rep (4188-4200)
         for d, L in [(64, 2), (32, 3)]:

@@ -1,0 +1,63 @@
+"""Deterministic MovieLens-shaped interaction data and BPR batches (pure numpy).
+
+Shared by tests/golden/make_train_golden.py (which trains the REFERENCE on it)
+and tests/test_gpu_training_parity.py (which trains igr on it): both sides
+see the same splits and the same (user, pos, neg) batches, so their
+trajectories can be compared step for step.
+
+The data is synthetic (no MovieLens files exist in the reference or the
+image): a rank-8 preference model with Zipf item popularity, per-user
+lognormal activity (>= 20 interactions, as ML's 20-rating minimum), then a
+per-user 80/10/10 split in (synthetic) time order - the shape of
+BasicDataset.generate_data (dataset.py:94-114) with split_ratio [0.8, 0.1, 0.1].
+"""
+import numpy as np
+
+SHAPES = {
+    # name: (n_users, n_items, mean interactions per user, d, n_layers, epochs)
+    'ml100k': (943, 1682, 106, 32, 1, 20),
+    'ml1m': (6040, 3706, 165, 64, 2, 10),
+}
+
+
+def make_splits(n_users, n_items, mean_deg, seed):
+    rng = np.random.default_rng(seed)
+    P = rng.normal(size=(n_users, 8))
+    Q = rng.normal(size=(n_items, 8))
+    pop = np.log(1.0 / np.arange(1, n_items + 1) ** 0.9)
+    rng.shuffle(pop)
+    logits = P @ Q.T / 2.0 + pop[None, :]
+    deg = np.clip(rng.lognormal(np.log(mean_deg) - 0.3, 0.8, n_users), 20, n_items // 2).astype(np.int64)
+    train, val, test = [], [], []
+    for u in range(n_users):
+        g = rng.gumbel(size=n_items)
+        items = np.argsort(-(logits[u] + g))[:deg[u]]
+        items = items[rng.permutation(len(items))]  # synthetic interaction time order
+        n_tr, n_te = int(len(items) * 0.8), int(len(items) * 0.1)
+        train.append(sorted(items[:n_tr].tolist()))
+        val.append(sorted(items[n_tr:len(items) - n_te].tolist()))
+        test.append(sorted(items[len(items) - n_te:].tolist()))
+    return train, val, test
+
+
+def batches(train_data, n_items, batch_size, n_steps, seed):
+    """n_steps batches of (users, pos, neg) with the distribution of
+    BasicDataset.__getitem__ (dataset.py:119-131)."""
+    rng = np.random.default_rng(seed)
+    users_ok = np.array([u for u in range(len(train_data)) if train_data[u]], np.int64)
+    sets = [set(x) for x in train_data]
+    out = []
+    for _ in range(n_steps):
+        u = users_ok[rng.integers(0, len(users_ok), batch_size)]
+        p = np.array([train_data[x][rng.integers(0, len(train_data[x]))] for x in u], np.int64)
+        n = rng.integers(0, n_items, batch_size)
+        for k in range(batch_size):
+            while n[k] in sets[u[k]]:
+                n[k] = rng.integers(0, n_items)
+        out.append((u, p, n))
+    return out
+
+
+def steps_per_epoch(train_data, batch_size):
+    n = sum(len(x) for x in train_data)
+    return (n + batch_size - 1) // batch_size

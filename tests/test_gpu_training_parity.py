@@ -1,0 +1,94 @@
+"""End-to-end training parity with the reference (Recall@20 within +-0.002).
+
+tests/golden/make_train_golden.py trained the REFERENCE IGCN (model.py +
+trainer.py loss code, CPU) on MovieLens-shaped data with fixed batches.  Here
+igr's IGCN + IGCNTrainer.step (fused HIP BPR kernels, HIP SpMM propagation)
+replays the same batches from the same initial embedding with the reference's
+CPU-generator dropout draws (dropout_rng='cpu'), and must reproduce the
+reference's per-epoch losses (rtol 5e-3: fp32 reassociation compounds through
+Adam over thousands of steps) and validation / test Recall@20 within the
+north-star bound of 0.002 at EVERY epoch.  With IGR_PARITY_OUT set, the
+trajectories are written there as JSON (profiles/ keeps the round's copy).
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from igr import model as M
+from igr import trainer as T
+
+sys.path.insert(0, GOLDEN)
+import ml_like  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda')
+
+
+class DS:
+    def __init__(self, name, n_users, n_items, train, val, test):
+        self.name, self.n_users, self.n_items, self.device = name, n_users, n_items, 'cpu'
+        self.train_data, self.val_data, self.test_data = train, val, test
+        self.train_array = [[u, i] for u in range(n_users) for i in train[u]]
+        self.train_pairs = np.array(self.train_array, dtype=np.int64)
+
+    def __len__(self):
+        return len(self.train_array)
+
+
+@pytest.mark.parametrize('shape', ['ml100k', 'ml1m'])
+def test_igcn_training_matches_reference(shape):
+    path = os.path.join(GOLDEN, f'train_{shape}.npz')
+    if not os.path.exists(path):
+        pytest.skip(f'{path} not generated')
+    ref = np.load(path)
+    nu, ni, mean_deg, d, L, epochs = ml_like.SHAPES[shape]
+    train, val, test = ml_like.make_splits(nu, ni, mean_deg, seed=100)
+    ds = DS(shape, nu, ni, train, val, test)
+    bs = 2048
+    spe = ml_like.steps_per_epoch(train, bs)
+    main_b = ml_like.batches(train, ni, bs, spe * epochs, seed=1)
+    aux_b = ml_like.batches(train, ni, bs, spe * epochs, seed=2)
+    torch.manual_seed(int(ref['seed']))
+    m = M.IGCN({'name': 'IGCN', 'embedding_size': d, 'n_layers': L, 'device': DEV, 'dropout': 0.3,
+                'feature_ratio': 1., 'dataset': ds, 'dropout_rng': 'cpu'})
+    e = m.embedding.weight.detach().double()
+    assert float(e.sum()) == pytest.approx(float(ref['init_sum']), rel=1e-12, abs=1e-9)
+    assert float(e.abs().sum()) == pytest.approx(float(ref['init_abs']), rel=1e-12)
+    tr = T.get_trainer({'name': 'IGCNTrainer', 'optimizer': 'Adam', 'lr': 1e-3, 'l2_reg': 0., 'aux_reg': 0.01,
+                        'device': DEV, 'n_epochs': epochs, 'batch_size': bs, 'test_batch_size': 512,
+                        'topks': [1, 5, 10, 15, 20]}, ds, m)
+    t = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    first = []
+    log = {'shape': shape, 'epochs': epochs, 'loss': [], 'loss_ref': ref['losses'].tolist(), 'val_recall20': [],
+           'val_recall20_ref': ref['val_recall20'].tolist(), 'test_recall20': [],
+           'test_recall20_ref': ref['test_recall20'].tolist()}
+    out = os.environ.get('IGR_PARITY_OUT')
+    for ep in range(epochs):
+        m.train()
+        tot = 0.
+        for s in range(spe):
+            u, p, n = main_b[ep * spe + s]
+            au, ap, an = aux_b[ep * spe + s]
+            loss = tr.step(t(u), t(p), t(n), t(au), t(ap), t(an)).item()
+            tot += loss
+            if ep == 0 and s < 20:
+                first.append(loss)
+        m.feat_mat_anneal()
+        _, vmet = tr.eval('val')
+        _, tmet = tr.eval('test')
+        log['loss'].append(tot / spe)
+        log['val_recall20'].append(float(vmet['Recall'][20]))
+        log['test_recall20'].append(float(tmet['Recall'][20]))
+        if out:
+            with open(os.path.join(out, f'training_parity_{shape}.json'), 'w') as f:
+                json.dump(log, f, indent=1)
+        np.testing.assert_allclose(tot / spe, ref['losses'][ep], rtol=5e-3)
+        assert abs(vmet['Recall'][20] - ref['val_recall20'][ep]) <= 0.002, (ep, vmet['Recall'][20], ref['val_recall20'][ep])
+        assert abs(tmet['Recall'][20] - ref['test_recall20'][ep]) <= 0.002, (ep, tmet['Recall'][20], ref['test_recall20'][ep])
+    np.testing.assert_allclose(first, ref['first_step_losses'], rtol=1e-4)
+    assert m.alpha == pytest.approx(float(ref['alpha_final']))

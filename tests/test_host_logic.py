@@ -96,3 +96,17 @@ def test_rank_nodes_degree(golden):
     A = O.generate_daj_mat(DS.n_users, DS.n_items, DS.train_pairs)
     deg = O.row_sums(A)
     assert np.all(np.diff(deg[ru]) <= 0) and np.all(np.diff(deg[DS.n_users + ri]) <= 0)
+
+
+def test_ngcf_graph_host_values_bit_exact(golden):
+    """NGCF.generate_graph (model.py:4009-4014): adj + I, l1 row-normalised."""
+    class DS:
+        n_users, n_items = int(golden['n_users']), int(golden['n_items'])
+        train_pairs = golden['train_array']
+    m = M.NGCF({'name': 'NGCF', 'embedding_size': 8, 'layer_sizes': [8], 'device': 'cpu', 'dropout': 0.1,
+                'dataset': DS()})
+    h = m.norm_adj.host()
+    np.testing.assert_array_equal(np.repeat(np.arange(m.norm_adj.n_rows), np.diff(h['row_ptr'])),
+                                  golden['ngcf_norm_idx'][0])
+    np.testing.assert_array_equal(h['col_idx'], golden['ngcf_norm_idx'][1])
+    np.testing.assert_array_equal(m.norm_vals.numpy(), golden['ngcf_norm_val'])

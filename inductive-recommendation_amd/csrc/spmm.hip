@@ -221,23 +221,34 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
     store_row4(epi, r, sub * 4, acc);
 }
 
-// Sum each split row's chunk partials in chunk order, then the epilogue.
+// Sum each split row's chunk partials, then the epilogue.  One workgroup per
+// split row: its 4*G lane groups ("slots") sum chunks slot, slot + 4G, ... in
+// order, then the slots are added in a fixed tree through LDS, so the result
+// is the same on every run whatever the chunk count (a row of 10^6 edges has
+// ~2000 chunks; a single group would walk them serially).
 template <int D>
 __global__ __launch_bounds__(256) void spmm_combine(const int32_t *__restrict__ split_row,
                                                     const int64_t *__restrict__ split_ptr,
                                                     int64_t n_split, const float *__restrict__ ws,
                                                     Epi epi) {
     constexpr int LPR = D / 4;
-    constexpr int G = 64 / LPR;
-    const int lane = threadIdx.x & 63;
-    const int grp = lane / LPR;
-    const int sub = lane - grp * LPR;
-    const int64_t i = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G + grp;
+    constexpr int S = 4 * (64 / LPR);  // slots per workgroup
+    __shared__ float4 red[S][LPR];
+    const int slot = threadIdx.x / LPR;
+    const int sub = threadIdx.x - slot * LPR;
+    const int64_t i = blockIdx.x;
     if (i >= n_split) return;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t c = split_ptr[i]; c < split_ptr[i + 1]; ++c)
+    for (int64_t c = split_ptr[i] + slot; c < split_ptr[i + 1]; c += S)
         acc = f4_add(acc, *reinterpret_cast<const float4 *>(ws + c * D + sub * 4));
-    store_row4(epi, split_row[i], sub * 4, acc);
+    red[slot][sub] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int w = S / 2; w >= 1; w >>= 1) {
+        if (slot < w) red[slot][sub] = f4_add(red[slot][sub], red[slot + w][sub]);
+        __syncthreads();
+    }
+    if (slot == 0) store_row4(epi, split_row[i], sub * 4, red[0][sub]);
 }
 
 // Any d / alignment: one wave per row, lanes over features.
@@ -272,11 +283,9 @@ static void launch_fast(const igr_csr *g, const float *x, int64_t ldx, const flo
                            g->row_ptr, g->col_idx, g->edge_id, rhs, x, ldx, g->order, g->n_order,
                            g->chunk_row, g->chunk_beg, g->n_chunks, g->chunk_edges, ws,
                            chunk_blocks, epi);
-    if (g->n_split > 0) {
-        const int64_t cb = (g->n_split + 4 * G - 1) / (4 * G);
-        hipLaunchKernelGGL((spmm_combine<D>), dim3((unsigned)cb), dim3(256), 0, st, g->split_row,
+    if (g->n_split > 0)
+        hipLaunchKernelGGL((spmm_combine<D>), dim3((unsigned)g->n_split), dim3(256), 0, st, g->split_row,
                            g->split_ptr, g->n_split, ws, epi);
-    }
 }
 
 template <int D>

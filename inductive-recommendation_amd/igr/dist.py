@@ -47,9 +47,17 @@ class BipartiteShard:
     pairs: all (user, item) interactions (every rank sees the same list);
     values follow utils.generate_daj_mat + LightGCN.generate_graph exactly
     (duplicates summed, fp32 degrees, numpy float32 pow, (dinv_r*a)*dinv_c).
+
+    The item block is cut two ways:
+      * row chunks (world > 1): each chunk's partial is all-reduced as soon as
+        its SpMM is done, so the exchange overlaps the remaining item chunks
+        and the user-side SpMM; only the last chunk's reduce is exposed;
+      * source tiles (large user tables): each pass gathers from a slice of
+        X[U_k] the Infinity Cache can hold, accumulating in place.
     """
 
-    def __init__(self, pairs, n_users, n_items, rank, world, device, degree=None, d=64, item_tiles='auto'):
+    def __init__(self, pairs, n_users, n_items, rank, world, device, degree=None, d=64, item_tiles='auto',
+                 item_chunks='auto'):
         self.n_users, self.n_items = n_users, n_items
         self.rank, self.world = rank, world
         u, i = pairs[:, 0], pairs[:, 1]
@@ -74,63 +82,92 @@ class BipartiteShard:
         # item block: rows = items, cols = local users
         rp2, ci2, v2, _ = csr_from_coo(li, lu, n_items, nu, None, dedup=True, want_eid=False)
         vals2 = sym_norm_values(rp2, ci2, v2, dinv_i, dinv_u)
-        self.item_block = Graph(rp2, ci2, n_items, nu, device=device)
-        self.item_vals = torch.from_numpy(vals2).to(device)
-        self.local_nnz = self.user_block.nnz + self.item_block.nnz
-        # Item rows gather the (large) user table: cut it into source tiles of
-        # ~640 MB so each pass gathers from a slice the Infinity Cache can hold,
-        # accumulating in place into the (small) item output.  Measured on MI355X
-        # at 10M x 1M, d = 64: 8.2 -> 7.7 ms (T = 4); more tiles cost more
-        # output passes than they save.
+        self.item_host = dict(row_ptr=rp2, col_idx=ci2, vals=vals2)
+        self.item_nnz = int(rp2[-1])
+        self.local_nnz = self.user_block.nnz + self.item_nnz
+        # source tiles: ~640 MB slices when the user table dwarfs the item output and the
+        # Infinity Cache (measured on MI355X at 10M x 1M, d = 64: 8.2 -> 7.7 ms at T = 4)
         T = item_tiles
         if T == 'auto':
             table, out = nu * d * 4, n_items * d * 4
             T = int(min(8, -(-table // (640 << 20)))) if table > 4 * max(out, MALL_BYTES) else 1
         self.item_tiles = max(1, int(T))
-        self.item_tiled = None
-        if self.item_tiles > 1:
-            b = [int(round(k * nu / self.item_tiles)) for k in range(self.item_tiles + 1)]
-            self.item_tiled = TiledGraph(self.item_block.host(), n_items, nu, b, device)
-            self.item_tile_vals = self.item_tiled.tile_values(self.item_vals)
+        C = item_chunks
+        if C == 'auto':
+            C = 4 if world > 1 else 1
+        self.item_chunks = max(1, int(C))
+        # row chunks with ~equal nnz, cut on the GLOBAL item degrees so every rank
+        # all-reduces the same row ranges
+        cuts = balanced_ranges(degree[n_users:], self.item_chunks)
+        col_bounds = [int(round(k * nu / self.item_tiles)) for k in range(self.item_tiles + 1)]
+        self.chunks = []  # (r0, r1, [(graph, vals, c0, c1), ...])
+        for r0, r1 in cuts:
+            e0, e1 = int(rp2[r0]), int(rp2[r1])
+            crp = (rp2[r0:r1 + 1] - e0).astype(np.int64)
+            cci = ci2[e0:e1]
+            cv = torch.from_numpy(vals2[e0:e1]).to(device)
+            if self.item_tiles == 1:
+                tiles = [(Graph(crp, cci, r1 - r0, nu, device=device), cv, 0, nu)]
+            else:
+                tg = TiledGraph(dict(row_ptr=crp, col_idx=cci), r1 - r0, nu, col_bounds, device)
+                tiles = [(g, v, col_bounds[t], col_bounds[t + 1]) for t, (g, v) in
+                         enumerate(zip(tg.tiles, tg.tile_values(cv)))]
+            self.chunks.append((r0, r1, tiles))
+
+    @property
+    def item_block(self):
+        """The whole item block as one Graph (built on first use; the layer uses the chunks)."""
+        if getattr(self, '_item_block', None) is None:
+            h = self.item_host
+            self._item_block = Graph(h['row_ptr'], h['col_idx'], self.n_items, self.u1 - self.u0,
+                                     device=self.user_block.device)
+        return self._item_block
+
+    @property
+    def item_vals(self):
+        """Values of the whole item block (CSR order), on the device."""
+        if getattr(self, '_item_vals', None) is None:
+            self._item_vals = torch.from_numpy(self.item_host['vals']).to(self.user_block.device)
+        return self._item_vals
 
     def launches(self):
         """The SpMM launches of one layer: (name, graph, source, n_rows, nnz)."""
         out = []
-        if self.item_tiled is not None:
-            for t, g in enumerate(self.item_tiled.tiles):
-                out.append((f'item{t}', g, 'users', g.n_rows, g.nnz))
-        else:
-            out.append(('item', self.item_block, 'users', self.item_block.n_rows, self.item_block.nnz))
+        for k, (r0, r1, tiles) in enumerate(self.chunks):
+            for t, (g, _, _, _) in enumerate(tiles):
+                out.append((f'item{k}.{t}', g, 'users', g.n_rows, g.nnz))
         out.append(('user', self.user_block, 'items', self.user_block.n_rows, self.user_block.nnz))
         return out
 
     def layer(self, x_users, x_items, y_users=None, y_items=None, group=None, spmm=None, hook=None):
         """One layer: returns (Y[U_k], Y[I]) with Y[I] all-reduced across ranks.
-        `spmm` defaults to the HIP kernel (the CPU gloo tests pass the oracle);
-        `hook(i, 'start'|'end')` brackets each SpMM launch (bench timing)."""
+
+        `spmm(g, x, vals, out, accumulate)` defaults to the HIP kernel (the CPU
+        gloo tests pass the oracle); `hook(i, 'start'|'end')` brackets each
+        SpMM launch (bench timing)."""
         hook = hook or (lambda i, ph: None)
-        if spmm is None and self.item_tiled is not None:
-            tg = self.item_tiled
-            if y_items is None:
-                y_items = torch.empty(self.n_items, x_users.shape[1], dtype=torch.float32, device=x_users.device)
-            for t, (g, v) in enumerate(zip(tg.tiles, self.item_tile_vals)):
-                hook(t, 'start')
-                ops.spmm(g, x_users[tg.bounds[t]:tg.bounds[t + 1]], v, out=y_items,
-                         epi=None if t == 0 else ops.epilogue(beta=1.0, add=y_items))
-                hook(t, 'end')
-            n_item = len(tg.tiles)
-        else:
-            spmm = ops.spmm if spmm is None else spmm
-            hook(0, 'start')
-            y_items = spmm(self.item_block, x_users, self.item_vals, out=y_items)
-            hook(0, 'end')
-            n_item = 1
-        work = None
-        if self.world > 1:
-            work = dist.all_reduce(y_items, op=dist.ReduceOp.SUM, group=group, async_op=True)
-        hook(n_item, 'start')
-        y_users = (spmm or ops.spmm)(self.user_block, x_items, self.user_vals, out=y_users)
-        hook(n_item, 'end')
-        if work is not None:
-            work.wait()
+        spmm = spmm or _hip_spmm
+        if y_items is None:
+            y_items = torch.empty(self.n_items, x_users.shape[1], dtype=torch.float32, device=x_users.device)
+        works, i = [], 0
+        for r0, r1, tiles in self.chunks:
+            yk = y_items[r0:r1]
+            for t, (g, v, c0, c1) in enumerate(tiles):
+                hook(i, 'start')
+                spmm(g, x_users[c0:c1], v, yk, t > 0)
+                hook(i, 'end')
+                i += 1
+            if self.world > 1:
+                works.append(dist.all_reduce(yk, op=dist.ReduceOp.SUM, group=group, async_op=True))
+        if y_users is None:
+            y_users = torch.empty(self.u1 - self.u0, x_items.shape[1], dtype=torch.float32, device=x_items.device)
+        hook(i, 'start')
+        spmm(self.user_block, x_items, self.user_vals, y_users, False)
+        hook(i, 'end')
+        for w in works:
+            w.wait()
         return y_users, y_items
+
+
+def _hip_spmm(g, x, vals, out, accumulate):
+    return ops.spmm(g, x, vals, out=out, epi=ops.epilogue(beta=1.0, add=out) if accumulate else None)

@@ -1,0 +1,75 @@
+"""IGCN training-step throughput on one GPU (reported in DESIGN.md, not the bench metric).
+
+One step = IGCNTrainer.step: device BPR sampling (main + aux batch), dropout
+of the feature values, inductive SpMM + L LightGCN SpMMs (fused layer mean),
+fused BPR + aux losses, the backward (L reverse SpMMs + transposed feature
+SpMM), fused Adam over the (N+2) x d table.  Synthetic uniform graph."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'inductive-recommendation_amd'))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--n-users', type=int, default=1_000_000)
+    ap.add_argument('--n-items', type=int, default=100_000)
+    ap.add_argument('--n-edges', type=int, default=20_000_000)
+    ap.add_argument('--d', type=int, default=64)
+    ap.add_argument('--layers', type=int, default=3)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=2048)
+    args = ap.parse_args()
+    from igr import model as M
+    from igr import trainer as T
+    from igr.dataset import synthetic_pairs
+    dev = torch.device('cuda')
+    pairs = synthetic_pairs(args.n_users, args.n_items, args.n_edges, 0)
+
+    class DS:
+        name = 'synthetic'
+        n_users, n_items, train_pairs = args.n_users, args.n_items, pairs
+        train_array = pairs
+        train_data = None
+
+        def __len__(self):
+            return len(pairs)
+    ds = DS()
+    t0 = time.time()
+    m = M.IGCN({'name': 'IGCN', 'embedding_size': args.d, 'n_layers': args.layers, 'device': dev, 'dropout': 0.3,
+                'feature_ratio': 1., 'dataset': ds})
+    # AuxiliaryDataset needs per-user lists; with feature_ratio = 1 it is the dataset itself
+    T.AuxiliaryDataset = lambda dataset, um, im: dataset
+    tr = T.get_trainer({'name': 'IGCNTrainer', 'optimizer': 'Adam', 'lr': 1e-3, 'l2_reg': 0., 'aux_reg': 0.01,
+                        'device': dev, 'n_epochs': 1, 'batch_size': args.batch, 'test_batch_size': 512,
+                        'topks': [20]}, ds, m)
+    print(f'built in {time.time() - t0:.1f}s: adj nnz {m.norm_adj.nnz}, feat nnz {m.feat_mat.nnz}', file=sys.stderr)
+    m.train()
+
+    def step():
+        u, p, n = tr.sampler.sample(args.batch)
+        au, ap_, an = tr.aux_sampler.sample(args.batch)
+        return tr.step(u, p, n, au, ap_, an)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    print(json.dumps({'ms_per_step': el / args.steps * 1e3, 'loss': float(loss), 'n_users': args.n_users,
+                      'n_items': args.n_items, 'n_edges': args.n_edges, 'd': args.d, 'layers': args.layers,
+                      'adj_nnz': m.norm_adj.nnz, 'feat_nnz': m.feat_mat.nnz,
+                      'edges_per_s_fwd_bwd': (m.norm_adj.nnz * args.layers + m.feat_mat.nnz) * 2 * args.steps / el}))
+
+
+if __name__ == '__main__':
+    main()

@@ -16,13 +16,14 @@ from igr.dist import BipartiteShard, balanced_ranges
 from oracle import igr_oracle as O
 
 
-def oracle_spmm(g, x, vals, out=None):
+def oracle_spmm(g, x, vals, out, accumulate):
     h = g.host()
     A = O.CSR(g.n_rows, g.n_cols, h['row_ptr'], h['col_idx'].astype(np.int64), vals.numpy())
-    y = torch.from_numpy(O.spmm(A, x.numpy()))
-    if out is None:
-        return y
-    out.copy_(y)
+    y = torch.from_numpy(O.spmm(A, np.ascontiguousarray(x.numpy())))
+    if accumulate:
+        out.add_(y)
+    else:
+        out.copy_(y)
     return out
 
 
@@ -34,17 +35,22 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, pairs, U, I, d, q):
+def _worker(rank, world, port, pairs, U, I, d, q, tiles=1, chunks='auto'):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        sh = BipartiteShard(pairs, U, I, rank, world, 'cpu')
+        sh = BipartiteShard(pairs, U, I, rank, world, 'cpu', item_tiles=tiles, item_chunks=chunks)
+        assert len(sh.chunks) == (4 if chunks == 'auto' else chunks)
         g = torch.Generator().manual_seed(0)
         xu_all = torch.randn(U, d, generator=g)
         xi = torch.randn(I, d, generator=g)
         yu, yi = sh.layer(xu_all[sh.u0:sh.u1].contiguous(), xi, spmm=oracle_spmm)
         q.put((rank, sh.u0, sh.u1, yu.numpy(), yi.numpy(), sh.local_nnz))
+    except Exception:
+        import traceback
+        q.put((rank, 'error', traceback.format_exc()))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -58,18 +64,22 @@ def test_balanced_ranges():
     assert max(loads) - min(loads) <= deg.max()
 
 
-@pytest.mark.parametrize('world', [2])
-def test_sharded_layer_matches_unsharded(world):
+@pytest.mark.parametrize('world,tiles,chunks', [(2, 1, 'auto'), (2, 3, 2)])
+def test_sharded_layer_matches_unsharded(world, tiles, chunks):
     U, I, E, d = 400, 150, 5000, 16
     rng = np.random.default_rng(0)
     pairs = np.stack([rng.integers(0, U, E), rng.integers(0, I, E)], 1)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, pairs, U, I, d, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, pairs, U, I, d, q, tiles, chunks))
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=120) for _ in range(world)])
+    res = [q.get(timeout=120) for _ in range(world)]
+    errs = [r[2] for r in res if r[1] == 'error']
+    assert not errs, errs[0]
+    res = sorted(res, key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -83,3 +93,13 @@ def test_sharded_layer_matches_unsharded(world):
         np.testing.assert_allclose(yu, y64[u0:u1], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(yi, y64[U:], rtol=1e-5, atol=1e-6)  # every rank holds the reduced items
     assert res[0][1] == 0 and res[-1][2] == U
+
+
+def test_item_chunks_identical_across_ranks():
+    """Every rank must all-reduce the same item row ranges (cut on global degrees)."""
+    U, I, E = 1000, 300, 8000
+    rng = np.random.default_rng(1)
+    pairs = np.stack([rng.integers(0, U, E), rng.integers(0, I, E)], 1)
+    cuts = [[(r0, r1) for r0, r1, _ in BipartiteShard(pairs, U, I, r, 4, 'cpu').chunks] for r in range(4)]
+    assert all(c == cuts[0] for c in cuts) and len(cuts[0]) == 4
+    assert cuts[0][0][0] == 0 and cuts[0][-1][1] == I

@@ -257,7 +257,7 @@ def test_bipartite_shard_tiled_items():
     rng = np.random.default_rng(14)
     pairs = np.stack([rng.integers(0, U, E), rng.integers(0, I, E)], 1)
     sh = BipartiteShard(pairs, U, I, 0, 1, DEV, item_tiles=3)
-    assert sh.item_tiled is not None and len(sh.launches()) == 4
+    assert sh.item_tiles == 3 and len(sh.chunks) == 1 and len(sh.launches()) == 4
     x = rng.standard_normal((U + I, d)).astype(np.float32)
     calls = []
     yu, yi = sh.layer(t(x[:U]), t(x[U:]), hook=lambda i, ph: calls.append((i, ph)))
@@ -265,6 +265,12 @@ def test_bipartite_shard_tiled_items():
     y64 = O.spmm64(O.norm_adj(U, I, pairs), x)
     close(yu.cpu().numpy(), y64[:U])
     close(yi.cpu().numpy(), y64[U:], atol_row=2e-6)
+    # row chunks x tiles (the multi-GPU layout, run here without a process group)
+    sh2 = BipartiteShard(pairs, U, I, 0, 1, DEV, item_tiles=2, item_chunks=3)
+    assert len(sh2.launches()) == 7
+    yu2, yi2 = sh2.layer(t(x[:U]), t(x[U:]))
+    close(yi2.cpu().numpy(), y64[U:], atol_row=2e-6)
+    close(yu2.cpu().numpy(), y64[:U])
 
 
 def test_fused_adam_matches_torch():

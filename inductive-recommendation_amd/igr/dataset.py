@@ -5,7 +5,8 @@ ProcessedDataset reads the same train/val/test.txt format
 sampler (dataset.py:119-131).  BPRBatchSampler draws whole batches with the
 same distribution in vectorised numpy (the reference runs the per-sample
 Python sampler in 6 DataLoader workers, trainer.py:522-526).
-SyntheticDataset builds the benchmark's random bipartite graphs.
+SyntheticDataset builds the benchmark's random bipartite graphs;
+GowallaDataset / MovieLensDataset ingest raw logs.
 """
 import os
 import random
@@ -82,6 +83,113 @@ def read_split(file_path):
             n_items = max(n_items, max(items) + 1)
         data.append(items)
     return data, n_items
+
+
+def ingest(raw_users, raw_items, times, min_inter, split_ratio):
+    """Vectorised restatement of the reference's raw pipeline:
+      remove_sparse_ui (dataset.py:66-92): iterative k-core on unique (user, item)
+        pairs - users with < min_inter items removed, then items with < min_inter
+        users, repeated until stable; survivors numbered in first-appearance order;
+      update_user_inter_lists (dataset.py:27-37): one entry per (user, item), the
+        earliest time, listed in first-appearance order;
+      generate_data (dataset.py:94-114): per-user stable sort by time, then
+        train = [:int(n*r0)], val = [int(n*r0):-int(n*r2)], test = [-int(n*r2):]
+        (with int(n*r2) == 0 the reference's slices give val = [] and test = the
+        whole list; kept as is).
+    Inputs are per-line arrays in file order; returns (train, val, test, n_users, n_items)."""
+    raw_users, raw_items = np.asarray(raw_users), np.asarray(raw_items)
+    times = np.asarray(times, np.int64)
+
+    def first_order_codes(x):
+        uniq, first, inv = np.unique(x, return_index=True, return_inverse=True)
+        rank = np.empty(len(uniq), np.int64)
+        rank[np.argsort(first, kind='stable')] = np.arange(len(uniq))
+        return rank[inv], len(uniq)
+    uc, nu0 = first_order_codes(raw_users)
+    ic, ni0 = first_order_codes(raw_items)
+    key = uc * ni0 + ic
+    ukey, kfirst = np.unique(key, return_index=True)
+    pu, pi = ukey // ni0, ukey % ni0
+    alive_u, alive_i = np.ones(nu0, bool), np.ones(ni0, bool)
+    live = np.ones(len(ukey), bool)
+    while True:
+        du = np.bincount(pu[live], minlength=nu0)
+        drop_u = alive_u & (du < min_inter)
+        alive_u &= ~drop_u
+        live &= alive_u[pu]
+        di = np.bincount(pi[live], minlength=ni0)
+        drop_i = alive_i & (di < min_inter)
+        alive_i &= ~drop_i
+        live &= alive_i[pi]
+        if not drop_u.any() and not drop_i.any():
+            break
+    umap = np.cumsum(alive_u) - 1
+    imap = np.cumsum(alive_i) - 1
+    n_users, n_items = int(alive_u.sum()), int(alive_i.sum())
+    # earliest time per kept pair; order = (user, time, first appearance of the pair)
+    pos = np.searchsorted(ukey, key)
+    tmin = np.full(len(ukey), np.iinfo(np.int64).max, np.int64)
+    np.minimum.at(tmin, pos, times)
+    sel = np.nonzero(live)[0]
+    order = np.lexsort((kfirst[sel], tmin[sel], umap[pu[sel]]))
+    sel = sel[order]
+    users, items = umap[pu[sel]], imap[pi[sel]]
+    ptr = np.searchsorted(users, np.arange(n_users + 1))
+    train, val, test = [], [], []
+    for u in range(n_users):
+        lst = items[ptr[u]:ptr[u + 1]].tolist()
+        k = len(lst)
+        n_tr, n_te = int(k * split_ratio[0]), int(k * split_ratio[2])
+        train.append(lst[:n_tr])
+        val.append(lst[n_tr:-n_te] if n_te else [])
+        test.append(lst[-n_te:] if n_te else lst)
+    return train, val, test, n_users, n_items
+
+
+class InteractionDataset(BasicDataset):
+    """Raw interaction logs -> train / val / test via `ingest` (the reference's
+    GowallaDataset pipeline); train_array is filled (the reference leaves it
+    empty and relies on ProcessedDataset re-reading the files it writes)."""
+
+    def load(self, raw_users, raw_items, times):
+        self.train_data, self.val_data, self.test_data, self.n_users, self.n_items = ingest(
+            raw_users, raw_items, times, self.config['min_inter'], self.config['split_ratio'])
+        self.train_array = [[u, i] for u in range(self.n_users) for i in self.train_data[u]]
+
+
+class GowallaDataset(InteractionDataset):
+    """dataset.py:167-189: Gowalla_totalCheckins.txt ('user<TAB>time<TAB>lat<TAB>lon<TAB>loc').
+    Times are parsed as UTC (the reference uses time.mktime: local time; only the
+    order matters, identical unless the host zone has DST jumps)."""
+
+    def __init__(self, dataset_config):
+        super().__init__(dataset_config)
+        import pandas as pd
+        df = pd.read_csv(os.path.join(dataset_config['path'], 'Gowalla_totalCheckins.txt'), sep='\t', header=None,
+                         names=['u', 't', 'lat', 'lon', 'i'], dtype={'u': np.int64, 't': str, 'i': np.int64})
+        t = pd.to_datetime(df['t'], format='%Y-%m-%dT%H:%M:%SZ', utc=True).astype('int64') // 10 ** 9
+        self.load(df['u'].to_numpy(), df['i'].to_numpy(), t.to_numpy())
+
+
+class MovieLensDataset(InteractionDataset):
+    """MovieLens ratings (no loader exists in the reference): ML-1M/10M
+    'ratings.dat' (user::movie::rating::time) or ML-100K 'u.data'
+    (tab-separated).  Ratings >= config['min_rating'] (default: all) are
+    interactions; the rest of the pipeline is the GowallaDataset one."""
+
+    def __init__(self, dataset_config):
+        super().__init__(dataset_config)
+        import pandas as pd
+        path = dataset_config['path']
+        f_dat, f_tab = os.path.join(path, 'ratings.dat'), os.path.join(path, 'u.data')
+        if os.path.exists(f_dat):
+            raw = pd.read_csv(f_dat, sep='::', header=None, engine='python').to_numpy(np.int64)
+        elif os.path.exists(f_tab):
+            raw = pd.read_csv(f_tab, sep='\t', header=None).to_numpy(np.int64)
+        else:
+            raise FileNotFoundError(f'no ratings.dat or u.data under {path}')
+        raw = raw[raw[:, 2] >= dataset_config.get('min_rating', -np.inf)]
+        self.load(raw[:, 0], raw[:, 1], raw[:, 3])
 
 
 class ProcessedDataset(BasicDataset):

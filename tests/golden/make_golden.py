@@ -348,6 +348,29 @@ def main():
                            'bytes': os.path.getsize(path)}
         print(cname, manifest[cname])
 
+    # --- raw ingestion: the reference's GowallaDataset (dataset.py:167-189) on a synthetic
+    # check-in file -> remove_sparse_ui + update_user_inter_lists + generate_data (dataset.py:66-114)
+    import tempfile
+    sys.path.insert(0, OUT)
+    import ml_like
+    import dataset as ref_dataset
+    os.environ['TZ'] = 'UTC'
+    import time as _time
+    _time.tzset()
+    with tempfile.TemporaryDirectory() as tmp:
+        ml_like.write_checkins(os.path.join(tmp, 'Gowalla_totalCheckins.txt'))
+        ig = {}
+        for tag, mi in [('k5', 5), ('k10', 10)]:
+            ds = ref_dataset.GowallaDataset({'name': 'GowallaDataset', 'path': tmp, 'device': 'cpu',
+                                             'min_inter': mi, 'split_ratio': [0.8, 0.1, 0.1]})
+            ig[f'{tag}_n'] = np.array([ds.n_users, ds.n_items], np.int64)
+            for split in ['train', 'val', 'test']:
+                data = getattr(ds, split + '_data')
+                ig[f'{tag}_{split}_ptr'] = np.cumsum([0] + [len(x) for x in data]).astype(np.int64)
+                ig[f'{tag}_{split}_items'] = np.array(sum(data, []), dtype=np.int64)
+        np.savez_compressed(os.path.join(OUT, 'ingest_gowalla.npz'), **ig)
+        print('ingest', {k: v.tolist() for k, v in ig.items() if k.endswith('_n')})
+
     manifest['_generator'] = {
         'reference': 'umaDosey/Inductive-Recommendation @ /root/reference (v1)',
         'torch': torch.__version__, 'numpy': np.__version__,

@@ -61,3 +61,20 @@ def batches(train_data, n_items, batch_size, n_steps, seed):
 def steps_per_epoch(train_data, batch_size):
     n = sum(len(x) for x in train_data)
     return (n + batch_size - 1) // batch_size
+
+
+def write_checkins(path, n_users=300, n_items=150, n_lines=9000, seed=21):
+    """A synthetic Gowalla_totalCheckins.txt ('user\\ttime\\tlat\\tlon\\tloc', dataset.py:173-186):
+    skewed activity so the k-core filter removes some users/items, repeated
+    check-ins (duplicates with different times) and timestamp ties."""
+    rng = np.random.default_rng(seed)
+    w_u = 1.0 / np.arange(1, n_users + 1) ** 0.8
+    w_i = 1.0 / np.arange(1, n_items + 1) ** 1.0
+    u = rng.choice(n_users, n_lines, p=w_u / w_u.sum()) * 7 + 3     # sparse raw ids
+    i = rng.choice(n_items, n_lines, p=w_i / w_i.sum()) * 11 + 5
+    t = 1262304000 + rng.integers(0, 3000, n_lines) * 600           # 2010-01-01 + 10-minute slots (ties)
+    import time as _t
+    with open(path, 'w') as f:
+        for a, b, c in zip(u, i, t):
+            ts = _t.strftime('%Y-%m-%dT%H:%M:%SZ', _t.gmtime(int(c)))
+            f.write(f'{a}\t{ts}\t30.2\t-97.7\t{b}\n')

@@ -1,4 +1,6 @@
 """Host-side logic of the model/trainer surface (CPU only)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -110,3 +112,45 @@ def test_ngcf_graph_host_values_bit_exact(golden):
                                   golden['ngcf_norm_idx'][0])
     np.testing.assert_array_equal(h['col_idx'], golden['ngcf_norm_idx'][1])
     np.testing.assert_array_equal(m.norm_vals.numpy(), golden['ngcf_norm_val'])
+
+
+@pytest.mark.parametrize('tag,min_inter', [('k5', 5), ('k10', 10)])
+def test_gowalla_ingestion_matches_reference(tmp_path, tag, min_inter):
+    """dataset.py:66-114 run by the reference on the same synthetic check-in file."""
+    import os
+    import sys
+    from conftest import GOLDEN
+    sys.path.insert(0, GOLDEN)
+    import ml_like
+    ml_like.write_checkins(os.path.join(tmp_path, 'Gowalla_totalCheckins.txt'))
+    ref = np.load(os.path.join(GOLDEN, 'ingest_gowalla.npz'))
+    ds = D.GowallaDataset({'name': 'GowallaDataset', 'path': str(tmp_path), 'device': 'cpu', 'min_inter': min_inter,
+                           'split_ratio': [0.8, 0.1, 0.1]})
+    assert [ds.n_users, ds.n_items] == ref[f'{tag}_n'].tolist()
+    for split in ['train', 'val', 'test']:
+        data = getattr(ds, split + '_data')
+        np.testing.assert_array_equal(np.cumsum([0] + [len(x) for x in data]), ref[f'{tag}_{split}_ptr'])
+        np.testing.assert_array_equal(np.array(sum(data, []), np.int64), ref[f'{tag}_{split}_items'])
+    # round trip through the ProcessedDataset files the reference consumes
+    ds.output_dataset(str(tmp_path / 'proc'))
+    p = D.ProcessedDataset({'name': 'ProcessedDataset', 'path': str(tmp_path / 'proc'), 'device': 'cpu'})
+    assert p.train_data == ds.train_data and p.n_users == ds.n_users
+
+
+def test_movielens_formats(tmp_path):
+    rows = [(1, 10, 5, 100), (1, 20, 3, 50), (2, 10, 4, 70), (2, 30, 1, 10), (1, 30, 4, 20)] * 1
+    with open(tmp_path / 'u.data', 'w') as f:
+        for r in rows:
+            f.write('\t'.join(map(str, r)) + '\n')
+    ds = D.MovieLensDataset({'name': 'MovieLensDataset', 'path': str(tmp_path), 'min_inter': 1,
+                             'split_ratio': [0.8, 0.1, 0.1]})
+    assert (ds.n_users, ds.n_items) == (2, 3)
+    # user 1: items by time: 30(20), 20(50), 10(100); n=3 -> train 2, test = whole list (quirk, n_test = 0)
+    assert ds.train_data[0] == [2, 1] and ds.val_data[0] == [] and ds.test_data[0] == [2, 1, 0]
+    os.makedirs(tmp_path / 'dat', exist_ok=True)
+    with open(tmp_path / 'dat' / 'ratings.dat', 'w') as f:
+        for r in rows:
+            f.write('::'.join(map(str, r)) + '\n')
+    d2 = D.MovieLensDataset({'name': 'MovieLensDataset', 'path': str(tmp_path / 'dat'), 'min_inter': 1,
+                             'split_ratio': [0.8, 0.1, 0.1], 'min_rating': 4})
+    assert d2.n_users == 2 and sum(len(x) for x in d2.train_data + d2.test_data) >= 3

@@ -71,12 +71,20 @@ __device__ __forceinline__ float4 f4_div(float4 a, float s) {
     return make_float4(a.x / s, a.y / s, a.z / s, a.w / s);
 }
 
-// Streamed-once loads (CSR structure, edge values): keep them out of the way
-// of the gathered feature table in L2 / Infinity Cache.
+// Streamed-once loads (CSR structure, edge values).  Measured on MI355X
+// (scripts/tune_spmm.py, 10M x 1M d=64): plain loads are 1-3 % faster than
+// non-temporal ones here, so IGR_NT_STREAM_LOADS is off by default.
+#ifdef IGR_NT_STREAM_LOADS
 template <class T>
 __device__ __forceinline__ T ld_stream(const T *p) {
     return __builtin_nontemporal_load(p);
 }
+#else
+template <class T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+    return *p;
+}
+#endif
 
 // Lane shuffle within the wave (ds_bpermute).
 __device__ __forceinline__ int shfl_i(int v, int src) { return __shfl(v, src, 64); }

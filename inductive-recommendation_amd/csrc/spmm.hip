@@ -21,8 +21,8 @@
 //  * Both tiers run in ONE launch (chunk blocks first, heaviest work first).
 //  * The row epilogue fuses the LightGCN/IGCN layer mean and the backward's
 //    "+ g/(L+1)" (igr_epilogue).
-//  * CSR structure and edge values are streamed with non-temporal loads so
-//    the gathered x table keeps the L2 / Infinity Cache.
+//  * CSR structure and edge values are plain loads (non-temporal loads and
+//    stores measured 1-3 % slower / neutral on MI355X, scripts/tune_spmm.py).
 #include <algorithm>
 
 #include "common.h"
@@ -42,6 +42,10 @@ struct Epi {
     int skip_y;
 };
 
+#ifndef IGR_SPMM_NT_STORE
+#define IGR_SPMM_NT_STORE 0
+#endif
+
 __device__ __forceinline__ void store_row4(const Epi &e, int64_t r, int f, float4 s) {
     float4 y = s;
     if (e.alpha != 1.f) y = f4_scale(e.alpha, y);
@@ -49,7 +53,16 @@ __device__ __forceinline__ void store_row4(const Epi &e, int64_t r, int f, float
         float4 a = *reinterpret_cast<const float4 *>(e.add + r * e.ld_add + f);
         y = f4_fma(e.beta, a, y);
     }
-    if (!e.skip_y) *reinterpret_cast<float4 *>(e.y + r * e.ldy + f) = y;
+    if (!e.skip_y) {
+        float4 *yp = reinterpret_cast<float4 *>(e.y + r * e.ldy + f);
+#if IGR_SPMM_NT_STORE
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v yv = {y.x, y.y, y.z, y.w};
+        __builtin_nontemporal_store(yv, reinterpret_cast<f4v *>(yp));
+#else
+        *yp = y;
+#endif
+    }
     if (e.acc_mode) {
         float4 *ap = reinterpret_cast<float4 *>(e.acc + r * e.ld_acc + f);
         float4 a = (e.acc_mode == 2) ? f4_add(*ap, y) : y;

@@ -143,6 +143,22 @@ int igr_plan_fill(int64_t n_rows, const int64_t *row_ptr, int64_t split_threshol
 int igr_spmm_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx, const float *rhs,
                  float *y, int64_t ldy, const igr_epilogue *epi, float *workspace, void *stream);
 
+/* SpMM with row / column scaled weights and fused dropout:
+ *   w(p) = (row_scale ? row_scale[r] : 1) * (col_scale ? col_scale[c] : 1)
+ *   if keep < 1: w = floor(keep + U) ? w / keep : 0,  U = uniform(seed, offset, edge id)
+ * The IGCN feature graph's values are row-constant (row_sum[r]^e,
+ * model.py:4127-4130), so its dropout SpMM (model.py:4016-4028, 4184) needs
+ * no per-edge array: forward uses row_scale, the reverse graph col_scale, and
+ * both draw the same mask from the forward edge id (the reverse graph's
+ * edge_id).  Same epilogue / workspace contract as igr_spmm_f32. */
+int igr_spmm_scaled_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx, const float *row_scale,
+                        const float *col_scale, float keep, uint64_t seed, uint64_t offset, float *y,
+                        int64_t ldy, const igr_epilogue *epi, float *workspace, void *stream);
+
+/* The uniforms igr_spmm_scaled_f32 draws for edge ids 0..n-1 (for tests and
+ * for an explicit-values replay of the same mask). */
+int igr_dropout_uniforms(int64_t n, uint64_t seed, uint64_t offset, float *out, void *stream);
+
 /* u_dot_v SDDMM: out[eid(p), h] = <u[row_p, h, :], v[col_p, h, :]>.
  * AttIGCN.masked_mm (model.py:4246-4255) with u = x_q (dst rows),
  * v = x_k (src rows); with h = 1 it is also the gspmm rhs-gradient.
@@ -159,12 +175,15 @@ int igr_segment_reduce_f32(const igr_csr *g, int32_t h, const float *x, int32_t 
 /* AttIGCN edge softmax, model.py:4270-4275, fused:
  *   m = segmax(alpha); a = exp((alpha - m[row]) / sqrt_d / 10); s = segsum(a);
  *   w[eid] = mean_h a / s[row]
+ * keep (nullable, [nnz] by edge id): edges with keep == 0 are treated as
+ * absent (dropout_sp_mat removes them from the reference's graph) - they
+ * enter neither max nor sum and get w = 0.
  * row_max / row_sum ([n_rows, h]) are saved for the backward. */
-int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alpha, float sqrt_d, float *w,
-                        float *row_max, float *row_sum, void *stream);
+int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alpha, const float *keep, float sqrt_d,
+                        float *w, float *row_max, float *row_sum, void *stream);
 /* Backward of igr_att_softmax_f32: dalpha[eid, h] from dw[eid]. */
-int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float *alpha, float sqrt_d,
-                            const float *row_max, const float *row_sum, const float *dw,
+int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float *alpha, const float *keep,
+                            float sqrt_d, const float *row_max, const float *row_sum, const float *dw,
                             float *dalpha, void *stream);
 
 /* NGCF.dropout_sp_mat (model.py:4016-4028) as a value mask over the fixed
@@ -173,7 +192,8 @@ int igr_edge_dropout_f32(int64_t n, const float *val, const float *rand, float p
                          void *stream);
 
 /* IGCN.update_feat_mat (model.py:4127-4130): out[p] = row_sum[row_p] ^ exponent,
- * exponent = (alpha - 1)/2 - 0.5 (= 1/sqrt for alpha = 1). */
+ * exponent = (alpha - 1)/2 - 0.5 (= 1/sqrt for alpha = 1).  With row_ptr ==
+ * NULL one value per row is written (out[r] = row_sum[r] ^ exponent). */
 int igr_feat_values_f32(int64_t n_rows, const int64_t *row_ptr, const float *row_sum,
                         float exponent, float *out, void *stream);
 

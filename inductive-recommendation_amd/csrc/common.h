@@ -86,6 +86,25 @@ __device__ __forceinline__ T ld_stream(const T *p) {
 }
 #endif
 
+// Counter-based random numbers: splitmix64 finaliser of (seed, offset, index).
+// A draw is a pure function of its counters, so a kernel needs no RNG state
+// and a backward pass can regenerate exactly the forward's draws.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t draw64(uint64_t seed, uint64_t offset, uint64_t i, uint32_t round) {
+    return mix64(mix64(seed ^ mix64(offset)) + (i << 8) + round);
+}
+
+// U[0, 1) with 24 random bits (the resolution of torch.rand for float32).
+__device__ __forceinline__ float uniform24(uint64_t seed, uint64_t offset, uint64_t i) {
+    return (float)(draw64(seed, offset, i, 0xD7) >> 40) * (1.0f / 16777216.0f);
+}
+
 // Lane shuffle within the wave (ds_bpermute).
 __device__ __forceinline__ int shfl_i(int v, int src) { return __shfl(v, src, 64); }
 __device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src, 64); }

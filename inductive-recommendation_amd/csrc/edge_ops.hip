@@ -108,9 +108,16 @@ __device__ __forceinline__ float att_exp(float a, float m, float sqrt_d) {
     return expf((a - m) / sqrt_d / 10.f);
 }
 
+// Edges whose keep value is 0 (dropped by dropout_sp_mat, model.py:4016-4028,
+// which REMOVES them from the reference's graph) take no part in the row max /
+// sum and get weight 0.
+__device__ __forceinline__ bool kept(const float *__restrict__ keep, int64_t e) {
+    return keep == nullptr || keep[e] != 0.f;
+}
+
 __global__ __launch_bounds__(256) void att_softmax_kernel(
     int64_t n_rows, int h, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
-    const float *__restrict__ alpha, float sqrt_d, float *__restrict__ w,
+    const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d, float *__restrict__ w,
     float *__restrict__ row_max, float *__restrict__ row_sum) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n_rows) return;
@@ -123,7 +130,9 @@ __global__ __launch_bounds__(256) void att_softmax_kernel(
         s[j] = 0.f;
     }
     for (int64_t p = b + lane; p < e; p += 64) {
-        const float *a = alpha + (eid ? eid[p] : p) * h;
+        const int64_t ed = eid ? eid[p] : p;
+        if (!kept(keep, ed)) continue;
+        const float *a = alpha + ed * h;
 #pragma unroll
         for (int j = 0; j < kMaxHeads; ++j)
             if (j < h) m[j] = fmaxf(m[j], a[j]);
@@ -132,7 +141,9 @@ __global__ __launch_bounds__(256) void att_softmax_kernel(
     for (int j = 0; j < kMaxHeads; ++j)
         if (j < h) m[j] = wave_max(m[j]);
     for (int64_t p = b + lane; p < e; p += 64) {
-        const float *a = alpha + (eid ? eid[p] : p) * h;
+        const int64_t ed = eid ? eid[p] : p;
+        if (!kept(keep, ed)) continue;
+        const float *a = alpha + ed * h;
 #pragma unroll
         for (int j = 0; j < kMaxHeads; ++j)
             if (j < h) s[j] += att_exp(a[j], m[j], sqrt_d);
@@ -148,6 +159,10 @@ __global__ __launch_bounds__(256) void att_softmax_kernel(
     }
     for (int64_t p = b + lane; p < e; p += 64) {
         const int64_t ed = eid ? eid[p] : p;
+        if (!kept(keep, ed)) {
+            w[ed] = 0.f;
+            continue;
+        }
         const float *a = alpha + ed * h;
         float acc = 0.f;
 #pragma unroll
@@ -162,7 +177,7 @@ __global__ __launch_bounds__(256) void att_softmax_kernel(
 // exactly-zero gradient (softmax is shift invariant) and is omitted.
 __global__ __launch_bounds__(256) void att_softmax_bwd_kernel(
     int64_t n_rows, int h, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
-    const float *__restrict__ alpha, float sqrt_d, const float *__restrict__ row_max,
+    const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d, const float *__restrict__ row_max,
     const float *__restrict__ row_sum, const float *__restrict__ dw, float *__restrict__ dalpha) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n_rows) return;
@@ -179,6 +194,7 @@ __global__ __launch_bounds__(256) void att_softmax_bwd_kernel(
     const float inv_h = 1.f / (float)h;
     for (int64_t p = b + lane; p < e; p += 64) {
         const int64_t ed = eid ? eid[p] : p;
+        if (!kept(keep, ed)) continue;
         const float g = dw[ed] * inv_h;
 #pragma unroll
         for (int j = 0; j < kMaxHeads; ++j)
@@ -190,11 +206,12 @@ __global__ __launch_bounds__(256) void att_softmax_bwd_kernel(
     const float c = sqrt_d * 10.f;
     for (int64_t p = b + lane; p < e; p += 64) {
         const int64_t ed = eid ? eid[p] : p;
+        const bool k = kept(keep, ed);
         const float g = dw[ed] * inv_h;
 #pragma unroll
         for (int j = 0; j < kMaxHeads; ++j)
             if (j < h) {
-                const float a = att_exp(alpha[ed * h + j], m[j], sqrt_d) / s[j];
+                const float a = k ? att_exp(alpha[ed * h + j], m[j], sqrt_d) / s[j] : 0.f;
                 dalpha[ed * h + j] = a * (g - S[j]) / c;
             }
     }
@@ -220,6 +237,10 @@ __global__ void feat_values_kernel(int64_t n_rows, const int64_t *__restrict__ r
         const float x = row_sum[r];
         // torch.pow(t, -0.5) lowers to rsqrt (1 / sqrt); other exponents to pow
         const float v = (ex == -0.5f) ? 1.f / sqrtf(x) : powf(x, ex);
+        if (!row_ptr) {
+            out[r] = v;
+            continue;
+        }
         for (int64_t p = row_ptr[r]; p < row_ptr[r + 1]; ++p) out[p] = v;
     }
 }
@@ -278,23 +299,23 @@ extern "C" int igr_segment_reduce_f32(const igr_csr *g, int32_t h, const float *
     });
 }
 
-extern "C" int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alpha, float sqrt_d,
-                                   float *w, float *row_max, float *row_sum, void *stream) {
+extern "C" int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alpha, const float *keep,
+                                   float sqrt_d, float *w, float *row_max, float *row_sum, void *stream) {
     return guarded("igr_att_softmax_f32", [&]() -> int {
         const char *fn = "igr_att_softmax_f32";
         if (!g || h <= 0 || h > kMaxHeads) return arg_error(fn, "h must be in [1, 8]");
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         hipLaunchKernelGGL(att_softmax_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0,
-                           st, g->n_rows, h, g->row_ptr, g->edge_id, alpha, sqrt_d, w, row_max,
+                           st, g->n_rows, h, g->row_ptr, g->edge_id, alpha, keep, sqrt_d, w, row_max,
                            row_sum);
         return launch_status(fn);
     });
 }
 
 extern "C" int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float *alpha,
-                                       float sqrt_d, const float *row_max, const float *row_sum,
-                                       const float *dw, float *dalpha, void *stream) {
+                                       const float *keep, float sqrt_d, const float *row_max,
+                                       const float *row_sum, const float *dw, float *dalpha, void *stream) {
     return guarded("igr_att_softmax_bwd_f32", [&]() -> int {
         const char *fn = "igr_att_softmax_bwd_f32";
         if (!g || h <= 0 || h > kMaxHeads) return arg_error(fn, "h must be in [1, 8]");
@@ -302,7 +323,7 @@ extern "C" int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float 
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         hipLaunchKernelGGL(att_softmax_bwd_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256),
-                           0, st, g->n_rows, h, g->row_ptr, g->edge_id, alpha, sqrt_d, row_max,
+                           0, st, g->n_rows, h, g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max,
                            row_sum, dw, dalpha);
         return launch_status(fn);
     });

@@ -81,17 +81,40 @@ __device__ __forceinline__ void store_row1(const Epi &e, int64_t r, int f, float
     }
 }
 
-template <bool VAL, bool EID>
-__device__ __forceinline__ float edge_weight(const float *__restrict__ val,
-                                             const int64_t *__restrict__ eid, int64_t p) {
-    if constexpr (!VAL) {
-        return 1.f;
-    } else if constexpr (EID) {
-        return val[ld_stream(eid + p)];
-    } else {
-        return ld_stream(val + p);
+// Edge-weight policies (template argument W of the kernels): the weight of
+// CSR position p of row r with source column c.
+struct W_One {  // rhs == NULL: unit weights
+    __device__ __forceinline__ float operator()(int64_t, int, int) const { return 1.f; }
+};
+struct W_Val {  // rhs by edge id == CSR position
+    const float *val;
+    __device__ __forceinline__ float operator()(int64_t p, int, int) const { return ld_stream(val + p); }
+};
+struct W_ValEid {  // rhs by edge id, edge id = edge_id[p] (multigraph / reverse graph)
+    const float *val;
+    const int64_t *eid;
+    __device__ __forceinline__ float operator()(int64_t p, int, int) const { return val[ld_stream(eid + p)]; }
+};
+// Row / column scaled weights with fused dropout (igr_spmm_scaled_f32):
+//   w = rs[r] * cs[c], then dropped (0) or divided by keep, the mask drawn from
+//   uniform24(seed, offset, edge id) so the reverse graph regenerates the
+//   forward's mask exactly.
+struct W_Scaled {
+    const float *rs, *cs;
+    const int64_t *eid;
+    float keep;
+    uint64_t seed, offset;
+    __device__ __forceinline__ float operator()(int64_t p, int c, int r) const {
+        float w = rs ? rs[r] : 1.f;
+        if (cs) w *= cs[c];
+        if (keep < 1.f) {
+            const int64_t e = eid ? ld_stream(eid + p) : p;
+            // random_tensor = keep + U; mask = floor(random_tensor) (model.py:4019-4021)
+            w = (floorf(keep + uniform24(seed, offset, (uint64_t)e)) != 0.f) ? w / keep : 0.f;
+        }
+        return w;
     }
-}
+};
 
 #ifndef IGR_SPMM_UNROLL
 #define IGR_SPMM_UNROLL 16
@@ -139,11 +162,10 @@ __device__ __forceinline__ float4 gather_block(float4 acc, int cl, float vl, int
     return acc;
 }
 
-template <int D, bool VAL, bool EID>
+template <int D, class W>
 __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
-    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
-    const int64_t *__restrict__ eid, const float *__restrict__ val, const float *__restrict__ x,
-    int64_t ldx, const int32_t *__restrict__ order, int64_t n_order,
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col, W wfn,
+    const float *__restrict__ x, int64_t ldx, const int32_t *__restrict__ order, int64_t n_order,
     const int32_t *__restrict__ chunk_row, const int64_t *__restrict__ chunk_beg, int64_t n_chunks,
     int64_t chunk_edges, float *__restrict__ ws, int64_t chunk_blocks, Epi epi) {
     constexpr int LPR = D / 4;   // lanes per feature row
@@ -169,7 +191,7 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
         float vl = 0.f;
         if (lane < n) {
             cl = ld_stream(col + base + lane);
-            vl = edge_weight<VAL, EID>(val, eid, base + lane);
+            vl = wfn(base + lane, cl, r);
         }
         while (n > 0) {
             const int64_t nb = base + 64;
@@ -178,7 +200,7 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
             float vl2 = 0.f;
             if (lane < nn) {
                 cl2 = ld_stream(col + nb + lane);
-                vl2 = edge_weight<VAL, EID>(val, eid, nb + lane);
+                vl2 = wfn(nb + lane, cl2, r);
             }
             // group grp takes edges [grp*LPR, grp*LPR + LPR) of this 64-edge block,
             // i.e. exactly the (col, val) pairs its own lanes loaded
@@ -214,7 +236,7 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
     float vl = 0.f;
     if (sub < n) {
         cl = ld_stream(col + base + sub);
-        vl = edge_weight<VAL, EID>(val, eid, base + sub);
+        vl = wfn(base + sub, cl, r);
     }
     while (n > 0) {
         const int64_t nb = base + LPR;
@@ -223,7 +245,7 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
         float vl2 = 0.f;
         if (sub < nn) {
             cl2 = ld_stream(col + nb + sub);
-            vl2 = edge_weight<VAL, EID>(val, eid, nb + sub);
+            vl2 = wfn(nb + sub, cl2, r);
         }
         acc = gather_block<U>(acc, cl, vl, gbase, n, xs, ldx);
         base = nb;
@@ -265,12 +287,10 @@ __global__ __launch_bounds__(256) void spmm_combine(const int32_t *__restrict__ 
 }
 
 // Any d / alignment: one wave per row, lanes over features.
-template <bool VAL, bool EID>
+template <class W>
 __global__ __launch_bounds__(256) void spmm_generic(int64_t n_rows, int d,
                                                     const int64_t *__restrict__ row_ptr,
-                                                    const int32_t *__restrict__ col,
-                                                    const int64_t *__restrict__ eid,
-                                                    const float *__restrict__ val,
+                                                    const int32_t *__restrict__ col, W wfn,
                                                     const float *__restrict__ x, int64_t ldx,
                                                     Epi epi) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -279,35 +299,89 @@ __global__ __launch_bounds__(256) void spmm_generic(int64_t n_rows, int d,
     const int64_t b = row_ptr[r], e = row_ptr[r + 1];
     for (int f = lane; f < d; f += 64) {
         float s = 0.f;
-        for (int64_t p = b; p < e; ++p) s = fmaf(edge_weight<VAL, EID>(val, eid, p), x[(int64_t)col[p] * ldx + f], s);
+        for (int64_t p = b; p < e; ++p) s = fmaf(wfn(p, col[p], (int)r), x[(int64_t)col[p] * ldx + f], s);
         store_row1(epi, r, f, s);
     }
 }
 
-template <int D, bool VAL, bool EID>
-static void launch_fast(const igr_csr *g, const float *x, int64_t ldx, const float *rhs,
-                        const Epi &epi, float *ws, hipStream_t st) {
+template <int D, class W>
+static void launch_fast(const igr_csr *g, const float *x, int64_t ldx, const W &wfn, const Epi &epi,
+                        float *ws, hipStream_t st) {
     constexpr int G = 64 / (D / 4);
     const int64_t chunk_blocks = (g->n_chunks + 3) / 4;
     const int64_t row_blocks = (g->n_order + 4 * G - 1) / (4 * G);
     const int64_t blocks = chunk_blocks + row_blocks;
     if (blocks > 0)
-        hipLaunchKernelGGL((spmm_main<D, VAL, EID>), dim3((unsigned)blocks), dim3(256), 0, st,
-                           g->row_ptr, g->col_idx, g->edge_id, rhs, x, ldx, g->order, g->n_order,
-                           g->chunk_row, g->chunk_beg, g->n_chunks, g->chunk_edges, ws,
-                           chunk_blocks, epi);
+        hipLaunchKernelGGL((spmm_main<D, W>), dim3((unsigned)blocks), dim3(256), 0, st, g->row_ptr, g->col_idx,
+                           wfn, x, ldx, g->order, g->n_order, g->chunk_row, g->chunk_beg, g->n_chunks,
+                           g->chunk_edges, ws, chunk_blocks, epi);
     if (g->n_split > 0)
         hipLaunchKernelGGL((spmm_combine<D>), dim3((unsigned)g->n_split), dim3(256), 0, st, g->split_row,
                            g->split_ptr, g->n_split, ws, epi);
 }
 
-template <int D>
-static void dispatch_fast(const igr_csr *g, const float *x, int64_t ldx, const float *rhs,
-                          const Epi &epi, float *ws, hipStream_t st) {
-    const bool val = rhs != nullptr, eid = g->edge_id != nullptr;
-    if (val && eid) launch_fast<D, true, true>(g, x, ldx, rhs, epi, ws, st);
-    else if (val) launch_fast<D, true, false>(g, x, ldx, rhs, epi, ws, st);
-    else launch_fast<D, false, false>(g, x, ldx, rhs, epi, ws, st);
+// Validate the epilogue / shapes, pick the fast (d in {32,64,128,256}, 16-B
+// aligned) or the generic kernel, and launch with the weight policy W.
+template <class W>
+static int run_spmm(const char *fn, const igr_csr *g, int32_t d, const float *x, int64_t ldx, const W &wfn,
+                    float *y, int64_t ldy, const igr_epilogue *epi_in, float *workspace, void *stream) {
+    if (!g) return arg_error(fn, "graph is NULL");
+    if (d <= 0) return arg_error(fn, "d must be positive");
+    if (g->n_rows < 0 || g->n_cols < 0 || g->nnz < 0) return arg_error(fn, "negative sizes");
+    if (g->n_rows == 0) return IGR_OK;
+    if (!g->row_ptr || (g->nnz > 0 && !g->col_idx)) return arg_error(fn, "missing CSR arrays");
+    if (g->nnz > 0 && !x) return arg_error(fn, "x is NULL");
+    if (ldx < d || ldy < d) return arg_error(fn, "leading dimension smaller than d");
+    if (g->n_order + g->n_split != g->n_rows)
+        return arg_error(fn, "schedule does not cover every row (n_order + n_split != n_rows)");
+    if (g->n_chunks > 0 && !workspace) return arg_error(fn, "workspace required for split rows");
+    Epi e{};
+    e.y = y;
+    e.ldy = ldy;
+    e.alpha = 1.f;
+    e.beta = 0.f;
+    e.acc_div = 1.f;
+    if (epi_in) {
+        e.alpha = epi_in->alpha;
+        e.beta = epi_in->beta;
+        e.add = epi_in->add;
+        e.ld_add = epi_in->ld_add;
+        e.acc = epi_in->acc;
+        e.ld_acc = epi_in->ld_acc;
+        e.acc_mode = epi_in->acc_mode;
+        e.acc_div = epi_in->acc_div;
+        e.skip_y = epi_in->skip_y;
+        if (e.acc_mode < 0 || e.acc_mode > 2) return arg_error(fn, "acc_mode must be 0, 1 or 2");
+        if (e.acc_mode && (!e.acc || e.ld_acc < d)) return arg_error(fn, "bad acc");
+        if (e.add && e.ld_add < d) return arg_error(fn, "bad ld_add");
+        if (e.acc_div == 0.f) return arg_error(fn, "acc_div is 0");
+    }
+    if (!e.skip_y && !y) return arg_error(fn, "y is NULL");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    bool fast = (d == 32 || d == 64 || d == 128 || d == 256) && (ldx % 4 == 0) && (ldy % 4 == 0) &&
+                aligned16(x) && aligned16(y) && aligned16(workspace);
+    if (e.add) fast = fast && aligned16(e.add) && e.ld_add % 4 == 0;
+    if (e.acc_mode) fast = fast && aligned16(e.acc) && e.ld_acc % 4 == 0;
+    if (fast) {
+        if (!g->order && g->n_order > 0) return arg_error(fn, "missing schedule");
+        switch (d) {
+            case 32: launch_fast<32>(g, x, ldx, wfn, e, workspace, st); break;
+            case 64: launch_fast<64>(g, x, ldx, wfn, e, workspace, st); break;
+            case 128: launch_fast<128>(g, x, ldx, wfn, e, workspace, st); break;
+            default: launch_fast<256>(g, x, ldx, wfn, e, workspace, st); break;
+        }
+    } else {
+        const unsigned blocks = (unsigned)((g->n_rows + 3) / 4);
+        hipLaunchKernelGGL((spmm_generic<W>), dim3(blocks), dim3(256), 0, st, g->n_rows, d, g->row_ptr, g->col_idx,
+                           wfn, x, ldx, e);
+    }
+    return launch_status(fn);
+}
+
+// The uniforms W_Scaled draws for edge ids 0..n-1 (tests / explicit-values path).
+__global__ void uniforms_kernel(int64_t n, uint64_t seed, uint64_t offset, float *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = uniform24(seed, offset, (uint64_t)i);
 }
 
 }  // namespace igr
@@ -315,69 +389,37 @@ static void dispatch_fast(const igr_csr *g, const float *x, int64_t ldx, const f
 using namespace igr;
 
 extern "C" int igr_spmm_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx,
-                            const float *rhs, float *y, int64_t ldy, const igr_epilogue *epi_in,
+                            const float *rhs, float *y, int64_t ldy, const igr_epilogue *epi,
                             float *workspace, void *stream) {
     return guarded("igr_spmm_f32", [&]() -> int {
         const char *fn = "igr_spmm_f32";
         if (!g) return arg_error(fn, "graph is NULL");
-        if (d <= 0) return arg_error(fn, "d must be positive");
-        if (g->n_rows < 0 || g->n_cols < 0 || g->nnz < 0) return arg_error(fn, "negative sizes");
-        if (g->n_rows == 0) return IGR_OK;
-        if (!g->row_ptr || (g->nnz > 0 && !g->col_idx)) return arg_error(fn, "missing CSR arrays");
-        if (g->nnz > 0 && !x) return arg_error(fn, "x is NULL");
-        if (ldx < d || ldy < d) return arg_error(fn, "leading dimension smaller than d");
-        if (g->n_order + g->n_split != g->n_rows)
-            return arg_error(fn, "schedule does not cover every row (n_order + n_split != n_rows)");
-        if (g->n_chunks > 0 && !workspace) return arg_error(fn, "workspace required for split rows");
-        Epi e{};
-        e.y = y;
-        e.ldy = ldy;
-        e.alpha = 1.f;
-        e.beta = 0.f;
-        e.acc_div = 1.f;
-        if (epi_in) {
-            e.alpha = epi_in->alpha;
-            e.beta = epi_in->beta;
-            e.add = epi_in->add;
-            e.ld_add = epi_in->ld_add;
-            e.acc = epi_in->acc;
-            e.ld_acc = epi_in->ld_acc;
-            e.acc_mode = epi_in->acc_mode;
-            e.acc_div = epi_in->acc_div;
-            e.skip_y = epi_in->skip_y;
-            if (e.acc_mode < 0 || e.acc_mode > 2) return arg_error(fn, "acc_mode must be 0, 1 or 2");
-            if (e.acc_mode && (!e.acc || e.ld_acc < d)) return arg_error(fn, "bad acc");
-            if (e.add && e.ld_add < d) return arg_error(fn, "bad ld_add");
-            if (e.acc_div == 0.f) return arg_error(fn, "acc_div is 0");
-        }
-        if (!e.skip_y && !y) return arg_error(fn, "y is NULL");
-        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        if (!rhs) return run_spmm(fn, g, d, x, ldx, W_One{}, y, ldy, epi, workspace, stream);
+        if (g->edge_id) return run_spmm(fn, g, d, x, ldx, W_ValEid{rhs, g->edge_id}, y, ldy, epi, workspace, stream);
+        return run_spmm(fn, g, d, x, ldx, W_Val{rhs}, y, ldy, epi, workspace, stream);
+    });
+}
 
-        bool fast = (d == 32 || d == 64 || d == 128 || d == 256) && (ldx % 4 == 0) &&
-                    (ldy % 4 == 0) && aligned16(x) && aligned16(y) && aligned16(workspace);
-        if (e.add) fast = fast && aligned16(e.add) && e.ld_add % 4 == 0;
-        if (e.acc_mode) fast = fast && aligned16(e.acc) && e.ld_acc % 4 == 0;
-        if (fast) {
-            if (!g->order && g->n_order > 0) return arg_error(fn, "missing schedule");
-            switch (d) {
-                case 32: dispatch_fast<32>(g, x, ldx, rhs, e, workspace, st); break;
-                case 64: dispatch_fast<64>(g, x, ldx, rhs, e, workspace, st); break;
-                case 128: dispatch_fast<128>(g, x, ldx, rhs, e, workspace, st); break;
-                default: dispatch_fast<256>(g, x, ldx, rhs, e, workspace, st); break;
-            }
-        } else {
-            const unsigned blocks = (unsigned)((g->n_rows + 3) / 4);
-            const bool val = rhs != nullptr, eid = g->edge_id != nullptr;
-            if (val && eid)
-                hipLaunchKernelGGL((spmm_generic<true, true>), dim3(blocks), dim3(256), 0, st, g->n_rows, d,
-                                   g->row_ptr, g->col_idx, g->edge_id, rhs, x, ldx, e);
-            else if (val)
-                hipLaunchKernelGGL((spmm_generic<true, false>), dim3(blocks), dim3(256), 0, st, g->n_rows, d,
-                                   g->row_ptr, g->col_idx, g->edge_id, rhs, x, ldx, e);
-            else
-                hipLaunchKernelGGL((spmm_generic<false, false>), dim3(blocks), dim3(256), 0, st, g->n_rows, d,
-                                   g->row_ptr, g->col_idx, g->edge_id, rhs, x, ldx, e);
-        }
-        return launch_status(fn);
+extern "C" int igr_spmm_scaled_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx,
+                                   const float *row_scale, const float *col_scale, float keep, uint64_t seed,
+                                   uint64_t offset, float *y, int64_t ldy, const igr_epilogue *epi,
+                                   float *workspace, void *stream) {
+    return guarded("igr_spmm_scaled_f32", [&]() -> int {
+        const char *fn = "igr_spmm_scaled_f32";
+        if (!g) return arg_error(fn, "graph is NULL");
+        if (!(keep > 0.f && keep <= 1.f)) return arg_error(fn, "keep must be in (0, 1]");
+        return run_spmm(fn, g, d, x, ldx, W_Scaled{row_scale, col_scale, g->edge_id, keep, seed, offset}, y, ldy,
+                        epi, workspace, stream);
+    });
+}
+
+extern "C" int igr_dropout_uniforms(int64_t n, uint64_t seed, uint64_t offset, float *out, void *stream) {
+    return guarded("igr_dropout_uniforms", [&]() -> int {
+        if (n <= 0) return IGR_OK;
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        int64_t blocks = (n + 255) / 256;
+        if (blocks > 16384) blocks = 16384;
+        hipLaunchKernelGGL(uniforms_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n, seed, offset, out);
+        return launch_status("igr_dropout_uniforms");
     });
 }

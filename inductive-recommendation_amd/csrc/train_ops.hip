@@ -11,16 +11,8 @@
 
 namespace igr {
 
-// splitmix64 finaliser: a counter-based generator, r = mix(seed, stream, index, round).
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
 __device__ __forceinline__ uint64_t draw(uint64_t seed, uint64_t offset, uint64_t i, uint32_t round) {
-    return mix64(mix64(seed ^ mix64(offset)) + (i << 8) + round);
+    return draw64(seed, offset, i, round);
 }
 
 // uniform integer in [0, n) from 64 random bits (Lemire's multiply-shift; bias < n / 2^64)

@@ -231,9 +231,20 @@ class IGCN(BasicModel):
         return g, vals
 
     def update_feat_mat(self):
-        """model.py:4127-4130: value = row_sum[row] ** ((alpha - 1)/2 - 0.5), on the device."""
+        """model.py:4127-4130: value = row_sum[row] ** ((alpha - 1)/2 - 0.5), on the device.
+        The value is row-constant, so one value per row (feat_base) is kept; the
+        per-edge array (feat_vals) is materialised only when asked for."""
         ex = (self.alpha - 1.) / 2. - 0.5
-        self.feat_vals = ops.feat_values(self.feat_mat, self.row_sum, ex)
+        self.feat_base = ops.feat_row_values(self.row_sum, ex)
+        self._feat_vals = None
+
+    @property
+    def feat_vals(self):
+        """Per-edge feature values (by edge id), as the reference's feat_mat.values()."""
+        if getattr(self, '_feat_vals', None) is None:
+            ex = (self.alpha - 1.) / 2. - 0.5
+            self._feat_vals = ops.feat_values(self.feat_mat, self.row_sum, ex)
+        return self._feat_vals
 
     def feat_mat_anneal(self):
         """model.py:4132-4134."""
@@ -277,10 +288,26 @@ class IGCN(BasicModel):
         return feat, user_map, item_map, row_sum
 
     def feat_values(self):
-        return dropout_values(self, self.feat_vals)
+        """Feature-graph weights for one get_rep (dropout_sp_mat, model.py:4189).
+
+        Default: ScaledWeights - row-constant values with the dropout mask drawn
+        inside the SpMM from a counter-based RNG (no rand tensor, no value
+        array; the backward regenerates the same mask).  dropout_rng = 'cpu'
+        instead materialises the values with the reference's own CPU-generator
+        draws (bit-for-bit the reference's mask)."""
+        if self.training and self.dropout > 0 and self.config.get('dropout_rng', 'device') == 'cpu':
+            return dropout_values(self, self.feat_vals)
+        if self.training and self.dropout > 0:
+            self._drop_step = getattr(self, '_drop_step', -1) + 1
+            if not hasattr(self, '_drop_seed'):
+                self._drop_seed = int(self.config.get('seed', torch.initial_seed())) & (2 ** 63 - 1)
+            return ops.ScaledWeights(self.feat_base, None, 1.0 - self.dropout, self._drop_seed, self._drop_step)
+        return ops.ScaledWeights(self.feat_base)
 
     def inductive_rep_layer(self, feat_vals):
         """model.py:4177-4186 (no padding needed: the lhs has n_cols rows)."""
+        if isinstance(feat_vals, ops.ScaledWeights):
+            return ops.propagate(self.norm_adj, self.embedding.weight, 0, feat=self.feat_mat, fvals=feat_vals)
         return ops.gspmm(self.feat_mat, 'mul', 'sum', self.embedding.weight, feat_vals)
 
     def get_rep(self):
@@ -355,12 +382,20 @@ class AttIGCN(IGCN):
         self.w = nn.Parameter(torch.ones([self.embedding_size], dtype=torch.float32, device=self.device))
         self.to(device=self.device)
 
+    def feat_values(self):
+        """Explicit per-edge dropout values: the attention layer needs them per edge."""
+        return dropout_values(self, self.feat_vals)
+
     def attention_values(self, feat_vals):
+        """model.py:4258-4275.  After dropout the dropped edges are absent from
+        the reference's graph; here they carry value 0 and are excluded from
+        the softmax through `keep`."""
         e = self.embedding.weight.detach()
         x_k = ops.linear(e, self.weight_k)
         x_q = ops.linear(ops.gspmm(self.feat_mat, 'mul', 'sum', e, feat_vals), self.weight_q)
         alpha = ops.gsddmm(self.feat_mat, 'dot', x_q, x_k, h=self.n_heads)
-        return ops.AttSoftmax.apply(self.feat_mat, alpha, ops.sqrt_scale(self.embedding_size))
+        keep = feat_vals if (self.training and self.dropout > 0) else None
+        return ops.AttSoftmax.apply(self.feat_mat, alpha, ops.sqrt_scale(self.embedding_size), keep)
 
     def inductive_rep_layer(self, feat_vals, return_alpha=False):
         w = self.attention_values(feat_vals)

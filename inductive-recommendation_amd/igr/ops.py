@@ -98,6 +98,64 @@ def spmm(g: Graph, x, rhs=None, out=None, epi=None):
     return out
 
 
+class ScaledWeights:
+    """Edge weights w = row_scale[r] * col_scale[c], dropout fused in-kernel with
+    keep probability `keep` and a counter-based mask keyed by (seed, offset,
+    edge id) - igr_spmm_scaled_f32.  For a graph whose values are row-constant
+    (the IGCN feature graph) this replaces the per-edge value array, the rand
+    tensor and the dropout pass."""
+
+    def __init__(self, row_scale=None, col_scale=None, keep=1.0, seed=0, offset=0):
+        self.row_scale, self.col_scale = row_scale, col_scale
+        self.keep, self.seed, self.offset = float(keep), int(seed), int(offset)
+
+    def transposed(self):
+        return ScaledWeights(self.col_scale, self.row_scale, self.keep, self.seed, self.offset)
+
+
+def spmm_scaled(g: Graph, x, w: ScaledWeights, out=None, epi=None):
+    """y = A_w x with ScaledWeights w (see igr_spmm_scaled_f32)."""
+    _dev(x, w.row_scale, w.col_scale, out)
+    x, ldx = _rows(x)
+    if x.shape[0] < g.n_cols:
+        raise IgrError(f'lhs has {x.shape[0]} rows, graph has {g.n_cols} source nodes')
+    if w.row_scale is not None and w.row_scale.numel() != g.n_rows:
+        raise IgrError('row_scale must have n_rows entries')
+    if w.col_scale is not None and w.col_scale.numel() != g.n_cols:
+        raise IgrError('col_scale must have n_cols entries')
+    d = x.shape[1]
+    if out is None:
+        out = torch.empty(g.n_rows, d, dtype=torch.float32, device=x.device)
+    L.call('igr_spmm_scaled_f32', ctypes.byref(g.csr), d, _p(x), ldx, _p(w.row_scale), _p(w.col_scale), w.keep,
+           ctypes.c_uint64(w.seed & (2 ** 64 - 1)), ctypes.c_uint64(w.offset & (2 ** 64 - 1)), _p(out),
+           out.stride(0), None if epi is None else ctypes.byref(epi), _p(g.workspace(d)), _stream())
+    return out
+
+
+def dropout_uniforms(n, seed, offset, device):
+    """The uniforms ScaledWeights' dropout draws for edge ids 0..n-1."""
+    out = torch.empty(n, dtype=torch.float32, device=device)
+    L.call('igr_dropout_uniforms', n, ctypes.c_uint64(seed & (2 ** 64 - 1)), ctypes.c_uint64(offset & (2 ** 64 - 1)),
+           _p(out), _stream())
+    return out
+
+
+def feat_row_values(row_sum, exponent):
+    """Per-row row_sum ** exponent (IGCN.update_feat_mat's value, model.py:4127-4130)."""
+    _dev(row_sum)
+    out = torch.empty_like(row_sum)
+    L.call('igr_feat_values_f32', row_sum.numel(), None, _p(row_sum), float(exponent), _p(out), _stream())
+    return out
+
+
+def _feat_spmm(feat, x, fw, out=None, epi=None, reverse=False):
+    """Feature-graph SpMM with per-edge values (tensor) or ScaledWeights."""
+    g = feat.reverse() if reverse else feat
+    if isinstance(fw, ScaledWeights):
+        return spmm_scaled(g, x, fw.transposed() if reverse else fw, out=out, epi=epi)
+    return spmm(g, x, fw, out=out, epi=epi)
+
+
 def sddmm_dot(g: Graph, u, v, h=1, out=None):
     """out[eid, j] = <u[row, j, :], v[col, j, :]>; u: [n_rows, h*d], v: [n_cols, h*d]."""
     _dev(u, v, out)
@@ -125,8 +183,9 @@ def segment_reduce(g: Graph, x, reduce='sum'):
     return out if x.dim() > 1 else out[:, 0]
 
 
-def att_softmax(g: Graph, alpha, sqrt_d):
-    _dev(alpha)
+def att_softmax(g: Graph, alpha, sqrt_d, keep=None):
+    """keep: optional [nnz] edge values; edges with keep == 0 are absent (dropped)."""
+    _dev(alpha, keep)
     alpha = _f32(alpha).contiguous()
     h = alpha.shape[1]
     if alpha.shape[0] != g.nnz:
@@ -134,16 +193,18 @@ def att_softmax(g: Graph, alpha, sqrt_d):
     w = torch.empty(g.nnz, dtype=torch.float32, device=alpha.device)
     rmax = torch.empty(g.n_rows, h, dtype=torch.float32, device=alpha.device)
     rsum = torch.empty_like(rmax)
-    L.call('igr_att_softmax_f32', ctypes.byref(g.csr), h, _p(alpha), float(sqrt_d), _p(w), _p(rmax), _p(rsum),
-           _stream())
+    keep = None if keep is None else keep.contiguous()
+    L.call('igr_att_softmax_f32', ctypes.byref(g.csr), h, _p(alpha), _p(keep), float(sqrt_d), _p(w), _p(rmax),
+           _p(rsum), _stream())
     return w, rmax, rsum
 
 
-def att_softmax_bwd(g: Graph, alpha, sqrt_d, rmax, rsum, dw):
-    _dev(alpha, dw)
+def att_softmax_bwd(g: Graph, alpha, sqrt_d, rmax, rsum, dw, keep=None):
+    _dev(alpha, dw, keep)
     dalpha = torch.empty_like(alpha)
-    L.call('igr_att_softmax_bwd_f32', ctypes.byref(g.csr), alpha.shape[1], _p(alpha), float(sqrt_d), _p(rmax),
-           _p(rsum), _p(dw.contiguous()), _p(dalpha), _stream())
+    keep = None if keep is None else keep.contiguous()
+    L.call('igr_att_softmax_bwd_f32', ctypes.byref(g.csr), alpha.shape[1], _p(alpha), _p(keep), float(sqrt_d),
+           _p(rmax), _p(rsum), _p(dw.contiguous()), _p(dalpha), _stream())
     return dalpha
 
 
@@ -269,19 +330,20 @@ class SegmentSum(torch.autograd.Function):
 
 
 class AttSoftmax(torch.autograd.Function):
-    """AttIGCN edge softmax + head mean (model.py:4270-4275)."""
+    """AttIGCN edge softmax + head mean (model.py:4270-4275); `keep` marks the
+    edges present after dropout (keep == 0: removed, as dropout_sp_mat does)."""
 
     @staticmethod
-    def forward(ctx, g, alpha, sqrt_d):
-        w, rmax, rsum = att_softmax(g, alpha, sqrt_d)
+    def forward(ctx, g, alpha, sqrt_d, keep=None):
+        w, rmax, rsum = att_softmax(g, alpha, sqrt_d, keep)
         ctx.g, ctx.sqrt_d = g, sqrt_d
-        ctx.save_for_backward(alpha, rmax, rsum)
+        ctx.save_for_backward(alpha, rmax, rsum, keep)
         return w
 
     @staticmethod
     def backward(ctx, dw):
-        alpha, rmax, rsum = ctx.saved_tensors
-        return None, att_softmax_bwd(ctx.g, alpha, ctx.sqrt_d, rmax, rsum, dw), None
+        alpha, rmax, rsum, keep = ctx.saved_tensors
+        return None, att_softmax_bwd(ctx.g, alpha, ctx.sqrt_d, rmax, rsum, dw, keep), None, None
 
 
 class Linear(torch.autograd.Function):
@@ -342,16 +404,18 @@ class Propagate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, adj, adj_vals, feat, emb, fvals, n_layers):
         ctx.adj, ctx.feat, ctx.L = adj, feat, n_layers
-        ctx.save_for_backward(adj_vals, fvals)
+        scaled = isinstance(fvals, ScaledWeights)
+        ctx.fw = fvals if scaled else None
+        ctx.save_for_backward(adj_vals, None if scaled else fvals)
         L1 = n_layers + 1
         dev = emb.device
-        ctx.emb = emb if (fvals is not None and fvals.requires_grad) else None
+        ctx.emb = emb if (not scaled and fvals is not None and fvals.requires_grad) else None
         if feat is not None:
             x = torch.empty(feat.n_rows, emb.shape[1], dtype=torch.float32, device=dev)
             if n_layers == 0:
-                return spmm(feat, emb, fvals, out=x)
+                return _feat_spmm(feat, emb, fvals, out=x)
             acc = torch.empty_like(x)
-            spmm(feat, emb, fvals, out=x, epi=epilogue(acc=acc, acc_mode=1))
+            _feat_spmm(feat, emb, fvals, out=x, epi=epilogue(acc=acc, acc_mode=1))
             own_x = True
         else:
             x = emb.contiguous()
@@ -372,6 +436,8 @@ class Propagate(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         adj_vals, fvals = ctx.saved_tensors
+        if ctx.fw is not None:
+            fvals = ctx.fw
         adj, feat, n_layers = ctx.adj, ctx.feat, ctx.L
         L1 = float(n_layers + 1)
         g = g.contiguous()
@@ -386,17 +452,16 @@ class Propagate(torch.autograd.Function):
                 dx, nxt = nxt, dx
         if feat is None:
             return None, None, None, dx, None, None
-        demb = spmm(feat.reverse(), dx, fvals) if ctx.needs_input_grad[3] else None
-        dfv = sddmm_dot(feat, dx, emb_saved(ctx), 1).view(-1) if ctx.needs_input_grad[4] else None
+        demb = _feat_spmm(feat, dx, fvals, reverse=True) if ctx.needs_input_grad[3] else None
+        dfv = None
+        if ctx.emb is not None and ctx.needs_input_grad[4]:
+            dfv = sddmm_dot(feat, dx, ctx.emb, 1).view(-1)
         return None, None, None, demb, dfv, None
 
 
-def emb_saved(ctx):
-    return ctx.emb
-
-
 def propagate(adj, emb, n_layers, feat=None, fvals=None, adj_vals=None):
-    """Fused get_rep: mean over [x0, A x0, ..., A^L x0], x0 = F emb (feat given) or emb."""
+    """Fused get_rep: mean over [x0, A x0, ..., A^L x0], x0 = F emb (feat given) or emb.
+    fvals: per-edge feature values (tensor, by edge id) or ScaledWeights."""
     return Propagate.apply(adj, adj_vals, feat, emb, fvals, n_layers)
 
 

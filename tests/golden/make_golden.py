@@ -312,6 +312,11 @@ def main():
             fx['att_alpha'] = m.inductive_rep_layer(m.feat_mat, return_alpha=True).numpy().copy()
             fx['att_x0'] = m.inductive_rep_layer(m.feat_mat).numpy().copy()
             fx['att_rep'] = m.get_rep().numpy().copy()
+            # train mode: dropout REMOVES edges before the softmax (model.py:4016-4028, 4265-4274)
+            m.train()
+            torch.manual_seed(33)
+            fx['att_train_rep'] = m.get_rep().numpy().copy()
+            m.eval()
 
         # --- eval + calculate_metrics (trainer.py:115-210) on the d=64 IGCN
         torch.manual_seed(200 + 64 + 2)

@@ -155,6 +155,26 @@ int igr_spmm_scaled_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx
                         const float *col_scale, float keep, uint64_t seed, uint64_t offset, float *y,
                         int64_t ldy, const igr_epilogue *epi, float *workspace, void *stream);
 
+/* Row-restricted SpMM and its transpose (training step: the loss reads the
+ * representation only at the batch rows, model.py:4048-4049 / 4049-4051, so
+ * the last layer of get_rep, model.py:4196 / 106, is needed only there and
+ * the first layer of its backward only pushes from there).  rows: int64
+ * [n_sel] row ids, repeats allowed; rhs: CSR-position values (NULL = 1;
+ * graphs with an edge_id permutation are not supported); d in {32, 64, 128,
+ * 256}; one workgroup per selected row, its lane groups striding the row.
+ *   igr_spmm_rows_f32: out[i] = scale * (sum_{p in row rows[i]} rhs[p] x[col[p]]
+ *                                        + add_g[rows[i]] + add_i[i])
+ *                      (add_g / add_i optional; fixed-order LDS reduction,
+ *                      deterministic)
+ *   igr_spmm_push_f32: dst[col[p]] += scale * rhs[p] * src[i] for p in row
+ *                      rows[i], and dst[rows[i]] += scale * src[i] when
+ *                      self_add (float atomics; summation order not fixed) */
+int igr_spmm_rows_f32(const igr_csr *g, int32_t d, const int64_t *rows, int64_t n_sel, const float *x, int64_t ldx,
+                      const float *rhs, const float *add_g, int64_t ld_g, const float *add_i, int64_t ld_i,
+                      float scale, float *out, int64_t ldo, void *stream);
+int igr_spmm_push_f32(const igr_csr *g, int32_t d, const int64_t *rows, int64_t n_sel, const float *src, int64_t lds,
+                      const float *rhs, float scale, int32_t self_add, float *dst, int64_t ldd, void *stream);
+
 /* The uniforms igr_spmm_scaled_f32 draws for edge ids 0..n-1 (for tests and
  * for an explicit-values replay of the same mask). */
 int igr_dropout_uniforms(int64_t n, uint64_t seed, uint64_t offset, float *out, void *stream);

@@ -63,6 +63,39 @@ def build_norm_adj(n_users, n_items, pairs, device):
     return g, torch.from_numpy(vals).to(device), degree, dinv
 
 
+def batch_edges_estimate(row_ptr, col_idx, n_users, batch_size):
+    """Expected adjacency edges the 3B rows of a BPR batch touch, under the
+    trainers' sampling: a uniform active user, a uniform item of that user, a
+    uniform item (sampler.py / dataset.BPRBatchSampler)."""
+    deg = np.diff(row_ptr).astype(np.float64)
+    ud = deg[:n_users]
+    active = np.nonzero(ud > 0)[0]
+    if len(active) == 0:
+        return 0.0
+    pos = np.add.reduceat(deg[col_idx[:row_ptr[n_users]]], row_ptr[:n_users][active]) / ud[active]
+    item = deg[n_users:].mean() if len(deg) > n_users else 0.0
+    return float(batch_size * (ud[active].mean() + pos.mean() + item))
+
+
+def batch_rep_pays(model, batch_size):
+    """Whether a BPR step should compute the last propagation layer only at the
+    batch rows (ops.propagate_rows) instead of over the whole graph.
+
+    model.config['batch_rep']: True / False, or 'auto' (default): take the row
+    path when the batch rows touch fewer than a quarter of the graph's edges
+    (batch_edges_estimate; the restricted forward + atomic push cost ~3-4x a
+    streamed edge)."""
+    mode = model.config.get('batch_rep', 'auto')
+    if mode != 'auto':
+        return bool(mode)
+    cache = model.__dict__.setdefault('_batch_rep_cache', {})
+    if batch_size not in cache:
+        h = model.norm_adj.host()
+        est = batch_edges_estimate(h['row_ptr'], h['col_idx'], model.n_users, batch_size)
+        cache[batch_size] = bool(4 * est < model.norm_adj.nnz)
+    return cache[batch_size]
+
+
 class BasicModel(nn.Module):
     """model.py:35-53."""
 
@@ -122,9 +155,16 @@ class LightGCN(BasicModel):
         return ops.gemm(users_r, rep[self.n_users:])
 
     def bpr_loss(self, users, pos_items, neg_items):
-        """Fused LightGCN/BPRTrainer step terms: (bpr loss, mean l2 of raw embeddings)."""
-        rep = self.get_rep()
-        bpr, _ = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
+        """Fused LightGCN/BPRTrainer step terms: (bpr loss, mean l2 of raw embeddings).
+        The last layer runs only at the batch rows when batch_rep_pays."""
+        if batch_rep_pays(self, users.numel()):
+            rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
+            rep_b = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
+                                       adj_vals=self.norm_vals)
+            bpr, _ = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0)
+        else:
+            rep = self.get_rep()
+            bpr, _ = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
         _, l2 = ops.bpr_loss(self.embedding.weight, users, pos_items, neg_items, 0, self.n_users)
         return bpr, l2
 
@@ -310,10 +350,14 @@ class IGCN(BasicModel):
             return ops.propagate(self.norm_adj, self.embedding.weight, 0, feat=self.feat_mat, fvals=feat_vals)
         return ops.gspmm(self.feat_mat, 'mul', 'sum', self.embedding.weight, feat_vals)
 
+    def inductive_values(self):
+        """Weights of the inductive layer for one get_rep (dropout applied in training)."""
+        return self.feat_values()
+
     def get_rep(self):
         """model.py:4188-4200, fused: inductive SpMM + L layers + layer mean."""
         return ops.propagate(self.norm_adj, self.embedding.weight, self.n_layers, feat=self.feat_mat,
-                             fvals=self.feat_values(), adj_vals=self.norm_vals)
+                             fvals=self.inductive_values(), adj_vals=self.norm_vals)
 
     def bpr_forward(self, users, pos_items, neg_items):
         return NGCF.bpr_forward(self, users, pos_items, neg_items)
@@ -322,7 +366,13 @@ class IGCN(BasicModel):
         return LightGCN.predict(self, users, rep)
 
     def bpr_loss(self, users, pos_items, neg_items):
-        """Fused IGCNTrainer terms on rep: (bpr loss, mean l2 of rep rows)."""
+        """Fused IGCNTrainer terms on rep: (bpr loss, mean l2 of rep rows).
+        The last layer runs only at the batch rows when batch_rep_pays."""
+        if batch_rep_pays(self, users.numel()):
+            rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
+            rep_b = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
+                                       feat=self.feat_mat, fvals=self.inductive_values(), adj_vals=self.norm_vals)
+            return ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0)
         rep = self.get_rep()
         return ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
 
@@ -354,6 +404,9 @@ class IMF(IGCN):
     def get_rep(self):
         return ops.propagate(self.norm_adj, self.embedding.weight, 0, feat=self.feat_mat,
                              fvals=self.feat_values(), adj_vals=self.norm_vals)
+
+    def bpr_loss(self, users, pos_items, neg_items):
+        return ops.bpr_loss(self.get_rep(), users, pos_items, neg_items, 0, self.n_users)
 
 
 class AttIGCN(IGCN):
@@ -403,10 +456,14 @@ class AttIGCN(IGCN):
             return w
         return ops.gspmm(self.feat_mat, 'mul', 'sum', self.embedding.weight, w)
 
-    def get_rep(self):
-        w = self.attention_values(self.feat_values())
-        return ops.propagate(self.norm_adj, self.embedding.weight, self.n_layers, feat=self.feat_mat, fvals=w,
-                             adj_vals=self.norm_vals)
+    def inductive_values(self):
+        return self.attention_values(self.feat_values())
+
+    def bpr_loss(self, users, pos_items, neg_items):
+        """IGCN.bpr_loss plus the projection norms bpr_forward adds to every
+        sample's l2 (model.py:4223-4287 text)."""
+        bpr, l2 = IGCN.bpr_loss(self, users, pos_items, neg_items)
+        return bpr, l2 + torch.norm(self.weight_q.weight, p=2) ** 2 + torch.norm(self.weight_k.weight, p=2) ** 2
 
     def bpr_forward(self, users, pos_items, neg_items):
         users_r, pos_r, neg_r, l2 = NGCF.bpr_forward(self, users, pos_items, neg_items)

@@ -459,6 +459,118 @@ class Propagate(torch.autograd.Function):
         return None, None, None, demb, dfv, None
 
 
+def spmm_rows(g: Graph, x, rows, rhs=None, add_g=None, add_i=None, scale=1.0, out=None):
+    """out[i] = scale * ((A x)[rows[i]] + add_g[rows[i]] + add_i[i]) (igr_spmm_rows_f32)."""
+    _dev(x, rows, rhs, add_g, add_i, out)
+    if g.edge_id is not None and rhs is not None:
+        raise IgrError('spmm_rows: rhs by edge id needs a graph without an edge_id permutation')
+    x, ldx = _rows(x)
+    d = x.shape[1]
+    rows = rows.to(torch.int64).contiguous()
+    if out is None:
+        out = torch.empty(rows.numel(), d, dtype=torch.float32, device=x.device)
+    ag, lg = _rows(add_g) if add_g is not None else (None, 0)
+    ai, li = _rows(add_i) if add_i is not None else (None, 0)
+    L.call('igr_spmm_rows_f32', ctypes.byref(g.csr), d, _p(rows), rows.numel(), _p(x), ldx,
+           _p(None if rhs is None else _f32(rhs).contiguous()), _p(ag), lg, _p(ai), li, float(scale), _p(out),
+           out.stride(0), _stream())
+    return out
+
+
+def spmm_push(g: Graph, rows, src, dst, rhs=None, scale=1.0, self_add=False):
+    """dst[col[p]] += scale * rhs[p] * src[i] for p in row rows[i] (+ dst[rows[i]] += scale * src[i])."""
+    _dev(src, rows, rhs, dst)
+    if g.edge_id is not None and rhs is not None:
+        raise IgrError('spmm_push: rhs by edge id needs a graph without an edge_id permutation')
+    src, lds = _rows(src)
+    rows = rows.to(torch.int64).contiguous()
+    if dst.stride(1) != 1 or dst.shape[1] != src.shape[1] or dst.shape[0] < g.n_cols:
+        raise IgrError('spmm_push: dst must be [n_cols, d] with unit inner stride')
+    L.call('igr_spmm_push_f32', ctypes.byref(g.csr), src.shape[1], _p(rows), rows.numel(), _p(src), lds,
+           _p(None if rhs is None else _f32(rhs).contiguous()), float(scale), int(bool(self_add)), _p(dst),
+           dst.stride(0), _stream())
+    return dst
+
+
+class PropagateRows(torch.autograd.Function):
+    """rep[rows] for Propagate's rep, computing the LAST layer only at `rows`.
+
+    Forward: x_0 .. x_{L-1} in full (no running-sum epilogue: the layer mean
+    is needed only at the rows), then one workgroup per selected row:
+        rep_b = ((A x_{L-1})[rows] + x_{L-1}[rows] + sum_{l<L-1} x_l[rows]) / (L+1).
+    Backward (g_b = d loss / d rep_b):
+        dx_{L-1} = push(A^T, g_b/(L+1)) + scatter(g_b/(L+1))    (atomic, sparse)
+        dx_l     = A^T dx_{l+1} + scatter(g_b/(L+1))            (full SpMM)
+        demb     = F^T dx_0
+    Two full-graph SpMMs fewer per training step than rep = Propagate(...)
+    followed by a gather; worth it when the batch rows touch far fewer edges
+    than the graph has (see model.batch_rep_pays)."""
+
+    @staticmethod
+    def forward(ctx, adj, adj_vals, feat, emb, fvals, n_layers, rows):
+        ctx.adj, ctx.feat, ctx.L = adj, feat, n_layers
+        scaled = isinstance(fvals, ScaledWeights)
+        ctx.fw = fvals if scaled else None
+        ctx.save_for_backward(adj_vals, None if scaled else fvals, rows)
+        ctx.emb = emb if (not scaled and fvals is not None and fvals.requires_grad) else None
+        ctx.n_emb = emb.shape[0]
+        L1 = n_layers + 1
+        x = _feat_spmm(feat, emb, fvals) if feat is not None else emb.contiguous()
+        s = None
+        for _ in range(n_layers - 1):
+            xr = gather_rows(x, rows)
+            s = xr if s is None else s.add_(xr)
+            x = spmm(adj, x, adj_vals)
+        return spmm_rows(adj, x, rows, adj_vals, add_g=x, add_i=s, scale=1.0 / L1)
+
+    @staticmethod
+    def backward(ctx, gb):
+        adj_vals, fvals, rows = ctx.saved_tensors
+        if ctx.fw is not None:
+            fvals = ctx.fw
+        adj, feat, n_layers = ctx.adj, ctx.feat, ctx.L
+        gs = gb.contiguous() / float(n_layers + 1)
+        dx = torch.zeros(adj.n_cols, gs.shape[1], dtype=torch.float32, device=gs.device)
+        spmm_push(adj, rows, gs, dx, adj_vals, self_add=True)
+        if n_layers > 1:
+            at = adj.reverse()
+            nxt = torch.empty_like(dx)
+            for _ in range(n_layers - 1):
+                spmm(at, dx, adj_vals, out=nxt)
+                scatter_add_rows(nxt, rows, gs)
+                dx, nxt = nxt, dx
+        if feat is None:
+            return None, None, None, dx, None, None, None
+        demb = _feat_spmm(feat, dx, fvals, reverse=True) if ctx.needs_input_grad[3] else None
+        dfv = None
+        if ctx.emb is not None and ctx.needs_input_grad[4]:
+            dfv = sddmm_dot(feat, dx, ctx.emb, 1).view(-1)
+        return None, None, None, demb, dfv, None, None
+
+
+def propagate_rows(adj, emb, n_layers, rows, feat=None, fvals=None, adj_vals=None):
+    """propagate(...)[rows] with the last layer computed only at `rows` (repeats allowed)."""
+    if n_layers == 0:
+        return gather(propagate(adj, emb, 0, feat, fvals, adj_vals), rows)
+    return PropagateRows.apply(adj, adj_vals, feat, emb, fvals, n_layers, rows.to(torch.int64).contiguous())
+
+
+_ARANGE = {}
+
+
+def batch_rows(users, pos, neg, n_users):
+    """Rows of rep a BPR batch reads, and the positions of (users, pos, neg) in
+    them: rows = [users, n_users + pos, n_users + neg] (repeats kept - no
+    host sync for a unique())."""
+    B = users.numel()
+    rows = torch.cat([users.to(torch.int64), pos.to(torch.int64) + n_users, neg.to(torch.int64) + n_users])
+    key = (B, users.device)
+    if key not in _ARANGE:
+        a = torch.arange(3 * B, dtype=torch.int64, device=users.device)
+        _ARANGE[key] = (a[:B], a[B:2 * B], a[2 * B:])
+    return rows, _ARANGE[key]
+
+
 def propagate(adj, emb, n_layers, feat=None, fvals=None, adj_vals=None):
     """Fused get_rep: mean over [x0, A x0, ..., A^L x0], x0 = F emb (feat given) or emb.
     fvals: per-edge feature values (tensor, by edge id) or ScaledWeights."""

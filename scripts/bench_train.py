@@ -3,7 +3,9 @@
 One step = IGCNTrainer.step: device BPR sampling (main + aux batch), dropout
 of the feature values, inductive SpMM + L LightGCN SpMMs (fused layer mean),
 fused BPR + aux losses, the backward (L reverse SpMMs + transposed feature
-SpMM), fused Adam over the (N+2) x d table.  Synthetic uniform graph."""
+SpMM), fused Adam over the (N+2) x d table.  Synthetic uniform graph.
+With batch_rep (default 'auto' -> taken here) the last forward layer and the
+first backward layer run only at the 3B batch rows (ops.propagate_rows)."""
 import argparse
 import json
 import os
@@ -26,6 +28,8 @@ def main():
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=2048)
+    ap.add_argument('--batch-rep', default='auto', choices=['auto', 'true', 'false'],
+                    help='last layer only at the batch rows (model.batch_rep_pays)')
     args = ap.parse_args()
     from igr import model as M
     from igr import trainer as T
@@ -44,7 +48,8 @@ def main():
     ds = DS()
     t0 = time.time()
     m = M.IGCN({'name': 'IGCN', 'embedding_size': args.d, 'n_layers': args.layers, 'device': dev, 'dropout': 0.3,
-                'feature_ratio': 1., 'dataset': ds})
+                'feature_ratio': 1., 'dataset': ds,
+                'batch_rep': {'auto': 'auto', 'true': True, 'false': False}[args.batch_rep]})
     # AuxiliaryDataset needs per-user lists; with feature_ratio = 1 it is the dataset itself
     T.AuxiliaryDataset = lambda dataset, um, im: dataset
     tr = T.get_trainer({'name': 'IGCNTrainer', 'optimizer': 'Adam', 'lr': 1e-3, 'l2_reg': 0., 'aux_reg': 0.01,
@@ -68,6 +73,7 @@ def main():
     print(json.dumps({'ms_per_step': el / args.steps * 1e3, 'loss': float(loss), 'n_users': args.n_users,
                       'n_items': args.n_items, 'n_edges': args.n_edges, 'd': args.d, 'layers': args.layers,
                       'adj_nnz': m.norm_adj.nnz, 'feat_nnz': m.feat_mat.nnz,
+                      'batch_rep': M.batch_rep_pays(m, args.batch),
                       'edges_per_s_fwd_bwd': (m.norm_adj.nnz * args.layers + m.feat_mat.nnz) * 2 * args.steps / el}))
 
 

@@ -318,3 +318,38 @@ def test_device_sampler_semantics():
     b = s.sample(1000, offset=7)
     c = s.sample(1000, offset=8)
     assert all(torch.equal(x, y) for x, y in zip(a, b)) and not torch.equal(a[2], c[2])
+
+
+@pytest.mark.parametrize('d', [32, 64, 128, 256])
+def test_spmm_rows_and_push_match_oracle(d):
+    """Row-restricted SpMM and its transpose (push), hub rows and repeated rows included."""
+    n = 900
+    g, v = rand_graph(n, n, 40000, seed=d + 1, skew=True)
+    rng = np.random.default_rng(d)
+    rows = rng.integers(0, n, 300)
+    rows[:20] = 0  # the hub row, repeated
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    ag = rng.standard_normal((n, d)).astype(np.float32)
+    ai = rng.standard_normal((300, d)).astype(np.float32)
+    y = ops.spmm_rows(g, t(x), t(rows), t(v), add_g=t(ag), add_i=t(ai), scale=0.25)
+    full = O.spmm64(oracle_csr(g, v), x)
+    close(y.cpu().numpy(), 0.25 * (full[rows] + ag[rows].astype(np.float64) + ai))
+    close(ops.spmm_rows(g, t(x), t(rows)).cpu().numpy(), O.spmm64(oracle_csr(g, np.ones_like(v)), x)[rows])
+    # push: dst += 0.5 * (A^T S + S), S[r] = sum of src[i] over rows[i] == r
+    src = rng.standard_normal((300, d)).astype(np.float32)
+    dst0 = rng.standard_normal((n, d)).astype(np.float32)
+    dst = ops.spmm_push(g, t(rows), t(src), t(dst0), t(v), scale=0.5, self_add=True).cpu().numpy()
+    h = g.host()
+    S = np.zeros((n, d))
+    np.add.at(S, rows, src.astype(np.float64))
+    erow = np.repeat(np.arange(n), np.diff(h['row_ptr']))
+    ref = S.copy()
+    np.add.at(ref, h['col_idx'], v.astype(np.float64)[:, None] * S[erow])
+    close(dst, dst0 + 0.5 * ref, atol_row=2e-6)
+
+
+def test_spmm_rows_rejects_edge_id_values():
+    g, v = rand_graph(50, 50, 400, seed=3, dedup=False)
+    assert g.edge_id is not None
+    with pytest.raises(ops.IgrError):
+        ops.spmm_rows(g, t(np.zeros((50, 32), np.float32)), t(np.arange(4)), t(v))

@@ -40,8 +40,11 @@ class DS:
         return len(self.train_array)
 
 
-@pytest.mark.parametrize('shape', ['ml100k', 'ml1m'])
-def test_igcn_training_matches_reference(shape):
+@pytest.mark.parametrize('shape,batch_rep', [('ml100k', 'auto'), ('ml1m', 'auto'), ('ml100k', True)])
+def test_igcn_training_matches_reference(shape, batch_rep):
+    """batch_rep True forces the row-restricted last layer (propagate_rows) on a
+    graph where 'auto' would not take it, so that path is pinned to the
+    reference's trajectory too."""
     path = os.path.join(GOLDEN, f'train_{shape}.npz')
     if not os.path.exists(path):
         pytest.skip(f'{path} not generated')
@@ -55,7 +58,7 @@ def test_igcn_training_matches_reference(shape):
     aux_b = ml_like.batches(train, ni, bs, spe * epochs, seed=2)
     torch.manual_seed(int(ref['seed']))
     m = M.IGCN({'name': 'IGCN', 'embedding_size': d, 'n_layers': L, 'device': DEV, 'dropout': 0.3,
-                'feature_ratio': 1., 'dataset': ds, 'dropout_rng': 'cpu'})
+                'feature_ratio': 1., 'dataset': ds, 'dropout_rng': 'cpu', 'batch_rep': batch_rep})
     e = m.embedding.weight.detach().double()
     assert float(e.sum()) == pytest.approx(float(ref['init_sum']), rel=1e-12, abs=1e-9)
     assert float(e.abs().sum()) == pytest.approx(float(ref['init_abs']), rel=1e-12)
@@ -85,7 +88,7 @@ def test_igcn_training_matches_reference(shape):
         log['val_recall20'].append(float(vmet['Recall'][20]))
         log['test_recall20'].append(float(tmet['Recall'][20]))
         if out:
-            with open(os.path.join(out, f'training_parity_{shape}.json'), 'w') as f:
+            with open(os.path.join(out, f'training_parity_{shape}' + ('_rows' if batch_rep is True else '') + '.json'), 'w') as f:
                 json.dump(log, f, indent=1)
         np.testing.assert_allclose(tot / spe, ref['losses'][ep], rtol=5e-3)
         assert abs(vmet['Recall'][20] - ref['val_recall20'][ep]) <= 0.002, (ep, vmet['Recall'][20], ref['val_recall20'][ep])

@@ -154,3 +154,15 @@ def test_movielens_formats(tmp_path):
     d2 = D.MovieLensDataset({'name': 'MovieLensDataset', 'path': str(tmp_path / 'dat'), 'min_inter': 1,
                              'split_ratio': [0.8, 0.1, 0.1], 'min_rating': 4})
     assert d2.n_users == 2 and sum(len(x) for x in d2.train_data + d2.test_data) >= 3
+
+
+def test_batch_edges_estimate_by_hand():
+    """2 users, 3 items: u0-{i0,i1}, u1-{i1}; bipartite adjacency rows 0-1 users, 2-4 items.
+    users: mean deg (2+1)/2; pos: u0 -> (deg i0 + deg i1)/2 = (1+2)/2, u1 -> deg i1 = 2
+    => mean 1.75; neg: mean item deg (1+2+0)/3."""
+    from igr import model as M
+    row = np.array([0, 0, 1, 2, 3, 3])
+    col = np.array([2, 3, 3, 0, 0, 1])
+    rp = np.searchsorted(row, np.arange(6)).astype(np.int64)
+    est = M.batch_edges_estimate(rp, col.astype(np.int32), 2, 10)
+    assert est == pytest.approx(10 * (1.5 + 1.75 + 1.0))

@@ -175,6 +175,27 @@ int igr_spmm_rows_f32(const igr_csr *g, int32_t d, const int64_t *rows, int64_t 
 int igr_spmm_push_f32(const igr_csr *g, int32_t d, const int64_t *rows, int64_t n_sel, const float *src, int64_t lds,
                       const float *rhs, float scale, int32_t self_add, float *dst, int64_t ldd, void *stream);
 
+/* The push without atomics (the training backward uses this one): mark the
+ * selected rows, sum repeated rows' sources into one slot each, then every
+ * output row gathers only from marked columns:
+ *   igr_rowset_mark:  bits[r/32] |= 1 << r%32, slot[r] = some i with rows[i] = r
+ *                     (bits zero on entry; bits: uint32[(n+31)/32], slot: int32[n])
+ *   igr_rowset_sum_f32: agg[slot[rows[i]]] += scale * src[i]   (agg zero on entry)
+ *   igr_spmm_pull_marked_f32: out[c] = scale * (sum_{p in row c, col[p] marked}
+ *                     rhs[p] agg[slot[col[p]]] + self_add [c marked] agg[slot[c]])
+ *                     (one lane group per row, fixed order: deterministic
+ *                     for distinct rows; repeats are summed into their slot
+ *                     with float atomics)
+ *   igr_rowset_clear: zero the words of bits holding the selected rows
+ * On the reverse graph, out = A^T G (+ G): igr_spmm_push_f32's result. */
+int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, int32_t *slot, void *stream);
+int igr_rowset_sum_f32(int64_t n_sel, int32_t d, const int64_t *rows, const int32_t *slot, const float *src,
+                       int64_t lds, float scale, float *agg, int64_t ld_agg, void *stream);
+int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint32_t *bits, const int32_t *slot, const float *agg,
+                             int64_t ld_agg, const float *rhs, float scale, int32_t self_add, float *out, int64_t ldo,
+                             void *stream);
+int igr_rowset_clear(int64_t n_sel, const int64_t *rows, uint32_t *bits, void *stream);
+
 /* The uniforms igr_spmm_scaled_f32 draws for edge ids 0..n-1 (for tests and
  * for an explicit-values replay of the same mask). */
 int igr_dropout_uniforms(int64_t n, uint64_t seed, uint64_t offset, float *out, void *stream);
@@ -231,12 +252,16 @@ int igr_scatter_add_rows_f32(int64_t n, int32_t d, const int64_t *idx, int64_t o
  *   s_b = sum_k u_k (n_k - p_k) * (w ? w_k : 1)
  *   loss[b] = softplus(s_b);  l2[b] = |u|^2 + |p|^2 + |n|^2      (loss/l2 nullable)
  * and, if grad != NULL, accumulates  g_loss * dloss_b/dt + g_l2 * dl2_b/dt
- * into grad (float atomics); if dw != NULL, g_loss * dloss_b/dw into dw.
- * (g_loss = dL/dloss_b, e.g. 1/batch for a mean.) */
+ * into grad (float atomics); if dw != NULL, g_loss * dloss_b/dw into dw
+ * (summed per workgroup in LDS first; d <= 1024).
+ * (g_loss = dL/dloss_b, e.g. 1/batch for a mean.)  g_loss_dev / g_l2_dev
+ * (nullable device scalars) multiply g_loss / g_l2: an autograd backward
+ * passes the incoming gradient without a device->host sync. */
 int igr_bpr_fwd_bwd_f32(int64_t batch, int32_t d, const int64_t *users, const int64_t *pos,
                         const int64_t *neg, int64_t off_u, int64_t off_i, const float *t,
                         int64_t ld_t, const float *w, float *loss, float *l2, float g_loss,
-                        float g_l2, float *grad, int64_t ld_grad, float *dw, void *stream);
+                        float g_l2, const float *g_loss_dev, const float *g_l2_dev, float *grad,
+                        int64_t ld_grad, float *dw, void *stream);
 
 /* Dense fp32 GEMM on MFMA (v_mfma_f32_16x16x4_f32, exact fp32 products):
  *   C[m, n] = sum_k A(m, k) * B(k, n) + bias[n]

@@ -365,16 +365,39 @@ class IGCN(BasicModel):
     def predict(self, users, rep=None):
         return LightGCN.predict(self, users, rep)
 
+    def _rows_path(self, batch_size):
+        return self.n_layers > 0 and batch_rep_pays(self, batch_size)
+
+    def _l2_extra(self):
+        return None
+
     def bpr_loss(self, users, pos_items, neg_items):
         """Fused IGCNTrainer terms on rep: (bpr loss, mean l2 of rep rows).
         The last layer runs only at the batch rows when batch_rep_pays."""
-        if batch_rep_pays(self, users.numel()):
+        if self._rows_path(users.numel()):
             rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
             rep_b = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
                                        feat=self.feat_mat, fvals=self.inductive_values(), adj_vals=self.norm_vals)
-            return ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0)
-        rep = self.get_rep()
-        return ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
+            bpr, l2 = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0)
+        else:
+            bpr, l2 = ops.bpr_loss(self.get_rep(), users, pos_items, neg_items, 0, self.n_users)
+        extra = self._l2_extra()
+        return bpr, (l2 if extra is None else l2 + extra)
+
+    def bpr_aux_loss(self, users, pos_items, neg_items, a_users, a_pos, a_neg):
+        """All three IGCNTrainer.step terms (trainer.py:536-549): (bpr, l2, aux).
+        On the row path the aux term rides in the same autograd node, so its
+        gradient is added into the embedding gradient in place."""
+        if not self._rows_path(users.numel()):
+            bpr, l2 = self.bpr_loss(users, pos_items, neg_items)
+            return bpr, l2, self.aux_loss(a_users, a_pos, a_neg)
+        rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
+        rep_b, aux = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
+                                        feat=self.feat_mat, fvals=self.inductive_values(), adj_vals=self.norm_vals,
+                                        aux=(a_users, a_pos, a_neg, len(self.user_map)), w=self.w)
+        bpr, l2 = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0)
+        extra = self._l2_extra()
+        return bpr, (l2 if extra is None else l2 + extra), aux
 
     def aux_loss(self, users, pos_items, neg_items):
         """IGCNTrainer aux term (trainer.py:542-549) on the raw feature table with w."""
@@ -405,8 +428,8 @@ class IMF(IGCN):
         return ops.propagate(self.norm_adj, self.embedding.weight, 0, feat=self.feat_mat,
                              fvals=self.feat_values(), adj_vals=self.norm_vals)
 
-    def bpr_loss(self, users, pos_items, neg_items):
-        return ops.bpr_loss(self.get_rep(), users, pos_items, neg_items, 0, self.n_users)
+    def _rows_path(self, batch_size):
+        return False  # the inductive layer alone: rep = F E
 
 
 class AttIGCN(IGCN):
@@ -459,11 +482,9 @@ class AttIGCN(IGCN):
     def inductive_values(self):
         return self.attention_values(self.feat_values())
 
-    def bpr_loss(self, users, pos_items, neg_items):
-        """IGCN.bpr_loss plus the projection norms bpr_forward adds to every
-        sample's l2 (model.py:4223-4287 text)."""
-        bpr, l2 = IGCN.bpr_loss(self, users, pos_items, neg_items)
-        return bpr, l2 + torch.norm(self.weight_q.weight, p=2) ** 2 + torch.norm(self.weight_k.weight, p=2) ** 2
+    def _l2_extra(self):
+        """The projection norms bpr_forward adds to every sample's l2 (model.py:4223-4287 text)."""
+        return torch.norm(self.weight_q.weight, p=2) ** 2 + torch.norm(self.weight_k.weight, p=2) ** 2
 
     def bpr_forward(self, users, pos_items, neg_items):
         users_r, pos_r, neg_r, l2 = NGCF.bpr_forward(self, users, pos_items, neg_items)

@@ -492,6 +492,41 @@ def spmm_push(g: Graph, rows, src, dst, rhs=None, scale=1.0, self_add=False):
     return dst
 
 
+def _rowset(g: Graph):
+    """Per-graph bitmap (zero between uses) + slot map over the column space."""
+    rs = getattr(g, '_rowset', None)
+    if rs is None:
+        n = g.n_cols
+        rs = (torch.zeros((n + 31) // 32, dtype=torch.int32, device=g.device),
+              torch.empty(max(n, 1), dtype=torch.int32, device=g.device))
+        g._rowset = rs
+    return rs
+
+
+def spmm_pull(g: Graph, rows, src, rhs=None, scale=1.0, self_add=False, out=None):
+    """out[c] = scale * (sum_{p in row c} rhs[p] S[col[p]] + self_add S[c]) with
+    S[r] = sum of src[i] over rows[i] == r - the atomic-free equivalent of
+    spmm_push on the reverse graph (igr_spmm_pull_marked_f32)."""
+    _dev(src, rows, rhs, out)
+    if g.edge_id is not None and rhs is not None:
+        raise IgrError('spmm_pull: rhs by edge id needs a graph without an edge_id permutation')
+    src, lds = _rows(src)
+    d = src.shape[1]
+    rows = rows.to(torch.int64).contiguous()
+    bits, slot = _rowset(g)
+    agg = torch.zeros(max(rows.numel(), 1), d, dtype=torch.float32, device=src.device)
+    if out is None:
+        out = torch.empty(g.n_rows, d, dtype=torch.float32, device=src.device)
+    st = _stream()
+    L.call('igr_rowset_mark', rows.numel(), _p(rows), _p(bits), _p(slot), st)
+    L.call('igr_rowset_sum_f32', rows.numel(), d, _p(rows), _p(slot), _p(src), lds, 1.0, _p(agg), agg.stride(0), st)
+    L.call('igr_spmm_pull_marked_f32', ctypes.byref(g.csr), d, _p(bits), _p(slot), _p(agg), agg.stride(0),
+           _p(None if rhs is None else _f32(rhs).contiguous()), float(scale), int(bool(self_add)), _p(out),
+           out.stride(0), st)
+    L.call('igr_rowset_clear', rows.numel(), _p(rows), _p(bits), st)
+    return out
+
+
 class PropagateRows(torch.autograd.Function):
     """rep[rows] for Propagate's rep, computing the LAST layer only at `rows`.
 
@@ -499,7 +534,7 @@ class PropagateRows(torch.autograd.Function):
     is needed only at the rows), then one workgroup per selected row:
         rep_b = ((A x_{L-1})[rows] + x_{L-1}[rows] + sum_{l<L-1} x_l[rows]) / (L+1).
     Backward (g_b = d loss / d rep_b):
-        dx_{L-1} = push(A^T, g_b/(L+1)) + scatter(g_b/(L+1))    (atomic, sparse)
+        dx_{L-1} = A^T G + G, G = scatter(g_b/(L+1))   (masked pull; push if A not symmetric)
         dx_l     = A^T dx_{l+1} + scatter(g_b/(L+1))            (full SpMM)
         demb     = F^T dx_0
     Two full-graph SpMMs fewer per training step than rep = Propagate(...)
@@ -507,31 +542,42 @@ class PropagateRows(torch.autograd.Function):
     than the graph has (see model.batch_rep_pays)."""
 
     @staticmethod
-    def forward(ctx, adj, adj_vals, feat, emb, fvals, n_layers, rows):
+    def forward(ctx, adj, adj_vals, feat, emb, fvals, n_layers, rows, aux=None, w=None):
         ctx.adj, ctx.feat, ctx.L = adj, feat, n_layers
+        ctx.aux = aux
         scaled = isinstance(fvals, ScaledWeights)
         ctx.fw = fvals if scaled else None
-        ctx.save_for_backward(adj_vals, None if scaled else fvals, rows)
+        ctx.save_for_backward(adj_vals, None if scaled else fvals, rows, emb if aux is not None else None, w)
         ctx.emb = emb if (not scaled and fvals is not None and fvals.requires_grad) else None
-        ctx.n_emb = emb.shape[0]
         L1 = n_layers + 1
+        aux_loss = None
+        if aux is not None:
+            au, ap, an, off = aux
+            loss = torch.empty(au.numel(), dtype=torch.float32, device=emb.device)
+            L.call('igr_bpr_fwd_bwd_f32', au.numel(), emb.shape[1], _p(au), _p(ap), _p(an), 0, int(off), _p(emb),
+                   emb.stride(0), _p(w), _p(loss), None, 0.0, 0.0, None, None, None, 0, None, _stream())
+            aux_loss = loss.mean()
         x = _feat_spmm(feat, emb, fvals) if feat is not None else emb.contiguous()
         s = None
         for _ in range(n_layers - 1):
             xr = gather_rows(x, rows)
             s = xr if s is None else s.add_(xr)
             x = spmm(adj, x, adj_vals)
-        return spmm_rows(adj, x, rows, adj_vals, add_g=x, add_i=s, scale=1.0 / L1)
+        rep_b = spmm_rows(adj, x, rows, adj_vals, add_g=x, add_i=s, scale=1.0 / L1)
+        return rep_b if aux is None else (rep_b, aux_loss)
 
     @staticmethod
-    def backward(ctx, gb):
-        adj_vals, fvals, rows = ctx.saved_tensors
+    def backward(ctx, gb, g_aux=None):
+        adj_vals, fvals, rows, emb, w = ctx.saved_tensors
         if ctx.fw is not None:
             fvals = ctx.fw
         adj, feat, n_layers = ctx.adj, ctx.feat, ctx.L
         gs = gb.contiguous() / float(n_layers + 1)
-        dx = torch.zeros(adj.n_cols, gs.shape[1], dtype=torch.float32, device=gs.device)
-        spmm_push(adj, rows, gs, dx, adj_vals, self_add=True)
+        if adj.reverse() is adj:
+            dx = spmm_pull(adj, rows, gs, adj_vals, self_add=True)
+        else:
+            dx = torch.zeros(adj.n_cols, gs.shape[1], dtype=torch.float32, device=gs.device)
+            spmm_push(adj, rows, gs, dx, adj_vals, self_add=True)
         if n_layers > 1:
             at = adj.reverse()
             nxt = torch.empty_like(dx)
@@ -539,20 +585,39 @@ class PropagateRows(torch.autograd.Function):
                 spmm(at, dx, adj_vals, out=nxt)
                 scatter_add_rows(nxt, rows, gs)
                 dx, nxt = nxt, dx
-        if feat is None:
-            return None, None, None, dx, None, None, None
-        demb = _feat_spmm(feat, dx, fvals, reverse=True) if ctx.needs_input_grad[3] else None
         dfv = None
-        if ctx.emb is not None and ctx.needs_input_grad[4]:
-            dfv = sddmm_dot(feat, dx, ctx.emb, 1).view(-1)
-        return None, None, None, demb, dfv, None, None
+        if feat is None:
+            demb = dx
+        else:
+            demb = _feat_spmm(feat, dx, fvals, reverse=True)
+            if ctx.emb is not None and ctx.needs_input_grad[4]:
+                dfv = sddmm_dot(feat, dx, ctx.emb, 1).view(-1)
+        dw = None
+        if ctx.aux is not None and g_aux is not None:
+            # the aux BPR term's gradient goes straight into demb (no second
+            # full-size gradient for autograd to add)
+            au, ap, an, off = ctx.aux
+            dw = torch.zeros_like(w) if (w is not None and ctx.needs_input_grad[8]) else None
+            g_aux = _f32(g_aux).contiguous()
+            L.call('igr_bpr_fwd_bwd_f32', au.numel(), emb.shape[1], _p(au), _p(ap), _p(an), 0, int(off), _p(emb),
+                   emb.stride(0), _p(w), None, None, 1.0 / au.numel(), 0.0, _p(g_aux), None, _p(demb),
+                   demb.stride(0), _p(dw), _stream())
+        return None, None, None, demb, dfv, None, None, None, dw
 
 
-def propagate_rows(adj, emb, n_layers, rows, feat=None, fvals=None, adj_vals=None):
-    """propagate(...)[rows] with the last layer computed only at `rows` (repeats allowed)."""
+def propagate_rows(adj, emb, n_layers, rows, feat=None, fvals=None, adj_vals=None, aux=None, w=None):
+    """propagate(...)[rows] with the last layer computed only at `rows` (repeats allowed).
+
+    aux = (users, pos, neg, off_i): also return the mean aux BPR loss on the
+    raw table emb with feature weights w (IGCNTrainer's aux term,
+    trainer.py:542-549); its gradient is accumulated into emb's gradient
+    inside the backward."""
     if n_layers == 0:
-        return gather(propagate(adj, emb, 0, feat, fvals, adj_vals), rows)
-    return PropagateRows.apply(adj, adj_vals, feat, emb, fvals, n_layers, rows.to(torch.int64).contiguous())
+        raise IgrError('propagate_rows needs n_layers >= 1')
+    if aux is not None:
+        aux = tuple(a.to(torch.int64).contiguous() for a in aux[:3]) + (int(aux[3]),)
+        _dev(*aux[:3], w)
+    return PropagateRows.apply(adj, adj_vals, feat, emb, fvals, n_layers, rows.to(torch.int64).contiguous(), aux, w)
 
 
 _ARANGE = {}
@@ -589,7 +654,7 @@ class BPRLoss(torch.autograd.Function):
         loss = torch.empty(B, dtype=torch.float32, device=t.device)
         l2 = torch.empty_like(loss)
         L.call('igr_bpr_fwd_bwd_f32', B, t.shape[1], _p(users), _p(pos), _p(neg), int(off_u), int(off_i), _p(t),
-               t.stride(0), _p(w), _p(loss), _p(l2), 0.0, 0.0, None, 0, None, _stream())
+               t.stride(0), _p(w), _p(loss), _p(l2), 0.0, 0.0, None, None, None, 0, None, _stream())
         ctx.save_for_backward(t, w, users, pos, neg)
         ctx.off = (int(off_u), int(off_i))
         return loss.mean(), l2.mean()
@@ -598,12 +663,14 @@ class BPRLoss(torch.autograd.Function):
     def backward(ctx, g_loss, g_l2):
         t, w, users, pos, neg = ctx.saved_tensors
         B = users.numel()
-        gl = float(g_loss) / B if g_loss is not None else 0.0
-        g2 = float(g_l2) / B if g_l2 is not None else 0.0
+        # incoming gradients stay on the device (no float() sync): the kernel scales by them
+        gl = None if g_loss is None else _f32(g_loss).contiguous()
+        g2 = None if g_l2 is None else _f32(g_l2).contiguous()
         grad = torch.zeros_like(t) if ctx.needs_input_grad[0] else None
         dw = torch.zeros_like(w) if (w is not None and ctx.needs_input_grad[1]) else None
         L.call('igr_bpr_fwd_bwd_f32', B, t.shape[1], _p(users), _p(pos), _p(neg), ctx.off[0], ctx.off[1], _p(t),
-               t.stride(0), _p(w), None, None, gl, g2, _p(grad), t.stride(0), _p(dw), _stream())
+               t.stride(0), _p(w), None, None, 0.0 if gl is None else 1.0 / B, 0.0 if g2 is None else 1.0 / B,
+               _p(gl), _p(g2), _p(grad), t.stride(0), _p(dw), _stream())
         return grad, dw, None, None, None, None, None
 
 

@@ -257,8 +257,7 @@ class IGCNTrainer(BasicTrainer):
     def step(self, users, pos_items, neg_items, a_users, a_pos, a_neg):
         m = self.model
         if self.fused:
-            bpr_loss, l2 = m.bpr_loss(users, pos_items, neg_items)
-            aux_loss = m.aux_loss(a_users, a_pos, a_neg)
+            bpr_loss, l2, aux_loss = m.bpr_aux_loss(users, pos_items, neg_items, a_users, a_pos, a_neg)
         else:
             users_r, pos_r, neg_r, l2_norm_sq = m.bpr_forward(users, pos_items, neg_items)
             bpr_loss = F.softplus(torch.sum(users_r * neg_r, 1) - torch.sum(users_r * pos_r, 1)).mean()

@@ -353,3 +353,40 @@ def test_spmm_rows_rejects_edge_id_values():
     assert g.edge_id is not None
     with pytest.raises(ops.IgrError):
         ops.spmm_rows(g, t(np.zeros((50, 32), np.float32)), t(np.arange(4)), t(v))
+
+
+@pytest.mark.parametrize('d', [32, 64, 128, 256])
+def test_spmm_pull_marked_equals_push(d):
+    """Atomic-free transpose (bitmap-masked pull) == A^T S + S, on a symmetric
+    graph with a hub, repeated rows, and a second call with other rows (the
+    bitmap must come back clean)."""
+    n = 1000
+    rng = np.random.default_rng(d + 7)
+    a = rng.integers(0, n, 20000)
+    b = rng.integers(0, n, 20000)
+    a[:3000] = 5  # hub
+    v = rng.standard_normal(20000).astype(np.float32)
+    g, vv = G.Graph.from_coo(np.concatenate([a, b]), np.concatenate([b, a]), n, n, np.concatenate([v, v]),
+                             dedup=True, device=DEV, symmetric=True)
+    assert g.reverse() is g
+    h = g.host()
+    erow = np.repeat(np.arange(n), np.diff(h['row_ptr']))
+    for trial in range(2):
+        rows = rng.integers(0, n, 257)
+        rows[:9] = 5 if trial == 0 else rows[9]
+        src = rng.standard_normal((257, d)).astype(np.float32)
+        y = ops.spmm_pull(g, t(rows), t(src), t(vv), scale=0.5, self_add=True).cpu().numpy()
+        S = np.zeros((n, d))
+        np.add.at(S, rows, src.astype(np.float64))
+        ref = S.copy()
+        np.add.at(ref, h['col_idx'], vv.astype(np.float64)[:, None] * S[erow])
+        close(y, 0.5 * ref, atol_row=2e-6)
+        push = ops.spmm_push(g, t(rows), t(src), torch.zeros(n, d, device=DEV), t(vv), scale=0.5, self_add=True)
+        close(y, push.cpu().numpy().astype(np.float64), atol_row=2e-6)
+        # deterministic for distinct rows (repeats are summed into their slot with float atomics)
+        u = np.unique(rows)
+        y1 = ops.spmm_pull(g, t(u), t(src[:len(u)]), t(vv), scale=0.5, self_add=True).cpu().numpy()
+        y2 = ops.spmm_pull(g, t(u), t(src[:len(u)]), t(vv), scale=0.5, self_add=True).cpu().numpy()
+        assert np.array_equal(y1, y2)
+    bits, _ = ops._rowset(g)
+    assert int(bits.abs().sum()) == 0

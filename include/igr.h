@@ -66,11 +66,14 @@ typedef struct igr_csr {
 } igr_csr;
 
 /* Fused row epilogue of a SpMM:
- *   y[r]   = alpha * (A x)[r] + beta * add[r]            (add may be NULL)
+ *   y[r]   = row_scale[r] * (alpha * (A x)[r] + beta * add[r])
+ *            (add, row_scale may be NULL)
  *   acc_mode 1: acc[r] = y[r] / acc_div
  *   acc_mode 2: acc[r] = (acc[r] + y[r]) / acc_div
  * It fuses the layer-mean of LightGCN/IGCN get_rep (model.py:108-109,
- * 4198-4199) and the "+ g/(L+1)" of its backward into the SpMM. */
+ * 4198-4199) and the "+ g/(L+1)" of its backward into the SpMM; row_scale
+ * lets the backward pre-scale dx_0 by the feature graph's row scale, so the
+ * transposed feature SpMM gathers no per-edge column scale. */
 typedef struct igr_epilogue {
     float alpha;
     float beta;
@@ -81,6 +84,8 @@ typedef struct igr_epilogue {
     int32_t acc_mode;
     float acc_div;
     int32_t skip_y;             /* 1: do not store y                             */
+    const float *row_scale;     /* [n_rows] or NULL: IGCN's feature row scale    */
+                                /* moved onto the reverse SpMM's source rows     */
 } igr_epilogue;
 
 /* ------------------------------------------------------------------ misc */

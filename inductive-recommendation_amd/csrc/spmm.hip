@@ -40,6 +40,7 @@ struct Epi {
     int acc_mode;
     float acc_div;
     int skip_y;
+    const float *row_scale;
 };
 
 #ifndef IGR_SPMM_NT_STORE
@@ -53,6 +54,7 @@ __device__ __forceinline__ void store_row4(const Epi &e, int64_t r, int f, float
         float4 a = *reinterpret_cast<const float4 *>(e.add + r * e.ld_add + f);
         y = f4_fma(e.beta, a, y);
     }
+    if (e.row_scale) y = f4_scale(e.row_scale[r], y);
     if (!e.skip_y) {
         float4 *yp = reinterpret_cast<float4 *>(e.y + r * e.ldy + f);
 #if IGR_SPMM_NT_STORE
@@ -74,6 +76,7 @@ __device__ __forceinline__ void store_row4(const Epi &e, int64_t r, int f, float
 __device__ __forceinline__ void store_row1(const Epi &e, int64_t r, int f, float s) {
     float y = e.alpha * s;
     if (e.add) y = fmaf(e.beta, e.add[r * e.ld_add + f], y);
+    if (e.row_scale) y *= e.row_scale[r];
     if (!e.skip_y) e.y[r * e.ldy + f] = y;
     if (e.acc_mode) {
         float a = (e.acc_mode == 2) ? e.acc[r * e.ld_acc + f] + y : y;
@@ -351,6 +354,7 @@ static int run_spmm(const char *fn, const igr_csr *g, int32_t d, const float *x,
         e.acc_mode = epi_in->acc_mode;
         e.acc_div = epi_in->acc_div;
         e.skip_y = epi_in->skip_y;
+        e.row_scale = epi_in->row_scale;
         if (e.acc_mode < 0 || e.acc_mode > 2) return arg_error(fn, "acc_mode must be 0, 1 or 2");
         if (e.acc_mode && (!e.acc || e.ld_acc < d)) return arg_error(fn, "bad acc");
         if (e.add && e.ld_add < d) return arg_error(fn, "bad ld_add");

@@ -34,7 +34,7 @@ class IgrEpilogue(ctypes.Structure):
     _fields_ = [
         ('alpha', c_f32), ('beta', c_f32), ('add', c_vp), ('ld_add', c_i64),
         ('acc', c_vp), ('ld_acc', c_i64), ('acc_mode', c_i32), ('acc_div', c_f32),
-        ('skip_y', c_i32),
+        ('skip_y', c_i32), ('row_scale', c_vp),
     ]
 
 

@@ -57,8 +57,11 @@ def _rows(t):
 
 # ------------------------------------------------------------------ raw ops
 
-def epilogue(alpha=1.0, beta=0.0, add=None, acc=None, acc_mode=0, acc_div=1.0, skip_y=False):
+def epilogue(alpha=1.0, beta=0.0, add=None, acc=None, acc_mode=0, acc_div=1.0, skip_y=False, row_scale=None):
     e = L.IgrEpilogue()
+    if row_scale is not None:
+        _f32(row_scale)
+        e.row_scale = row_scale.data_ptr()
     e.alpha, e.beta = alpha, beta
     if add is not None:
         e.add, e.ld_add = add.data_ptr(), add.stride(0)
@@ -154,6 +157,23 @@ def _feat_spmm(feat, x, fw, out=None, epi=None, reverse=False):
     if isinstance(fw, ScaledWeights):
         return spmm_scaled(g, x, fw.transposed() if reverse else fw, out=out, epi=epi)
     return spmm(g, x, fw, out=out, epi=epi)
+
+
+def _prescale(fw):
+    """Row scale to fold into dx_0 before the transposed feature SpMM (None
+    unless fw is ScaledWeights with a row scale only): F^T diag(s) M dx =
+    F^T M (s * dx), so the reverse SpMM draws the mask but gathers no per-edge
+    column scale."""
+    if isinstance(fw, ScaledWeights) and fw.row_scale is not None and fw.col_scale is None:
+        return fw.row_scale
+    return None
+
+
+def _feat_spmm_rev(feat, dx, fw, prescaled):
+    """demb = F_w^T dx; `prescaled` means dx already carries fw's row scale."""
+    if prescaled:
+        return spmm_scaled(feat.reverse(), dx, ScaledWeights(None, None, fw.keep, fw.seed, fw.offset))
+    return _feat_spmm(feat, dx, fw, reverse=True)
 
 
 def sddmm_dot(g: Graph, u, v, h=1, out=None):
@@ -441,18 +461,20 @@ class Propagate(torch.autograd.Function):
         adj, feat, n_layers = ctx.adj, ctx.feat, ctx.L
         L1 = float(n_layers + 1)
         g = g.contiguous()
+        rs = _prescale(fvals) if (feat is not None and ctx.needs_input_grad[3]) else None
         if n_layers == 0:
-            dx = g
+            dx = g if rs is None else g * rs[:, None]
         else:
             dx = g / L1
             at = adj.reverse()
             nxt = torch.empty_like(dx)
-            for _ in range(n_layers):
-                spmm(at, dx, adj_vals, out=nxt, epi=epilogue(beta=1.0 / L1, add=g))
+            for layer in range(n_layers):
+                last = layer == n_layers - 1
+                spmm(at, dx, adj_vals, out=nxt, epi=epilogue(beta=1.0 / L1, add=g, row_scale=rs if last else None))
                 dx, nxt = nxt, dx
         if feat is None:
             return None, None, None, dx, None, None
-        demb = _feat_spmm(feat, dx, fvals, reverse=True) if ctx.needs_input_grad[3] else None
+        demb = _feat_spmm_rev(feat, dx, fvals, rs is not None) if ctx.needs_input_grad[3] else None
         dfv = None
         if ctx.emb is not None and ctx.needs_input_grad[4]:
             dfv = sddmm_dot(feat, dx, ctx.emb, 1).view(-1)
@@ -573,6 +595,7 @@ class PropagateRows(torch.autograd.Function):
             fvals = ctx.fw
         adj, feat, n_layers = ctx.adj, ctx.feat, ctx.L
         gs = gb.contiguous() / float(n_layers + 1)
+        rs = _prescale(fvals) if feat is not None else None
         if adj.reverse() is adj:
             dx = spmm_pull(adj, rows, gs, adj_vals, self_add=True)
         else:
@@ -581,15 +604,18 @@ class PropagateRows(torch.autograd.Function):
         if n_layers > 1:
             at = adj.reverse()
             nxt = torch.empty_like(dx)
-            for _ in range(n_layers - 1):
-                spmm(at, dx, adj_vals, out=nxt)
-                scatter_add_rows(nxt, rows, gs)
+            for layer in range(n_layers - 1):
+                last = layer == n_layers - 2
+                spmm(at, dx, adj_vals, out=nxt, epi=epilogue(row_scale=rs) if (last and rs is not None) else None)
+                scatter_add_rows(nxt, rows, gs if not (last and rs is not None) else gs * rs[rows][:, None])
                 dx, nxt = nxt, dx
+        elif rs is not None:
+            dx.mul_(rs[:, None])
         dfv = None
         if feat is None:
             demb = dx
         else:
-            demb = _feat_spmm(feat, dx, fvals, reverse=True)
+            demb = _feat_spmm_rev(feat, dx, fvals, rs is not None)
             if ctx.emb is not None and ctx.needs_input_grad[4]:
                 dfv = sddmm_dot(feat, dx, ctx.emb, 1).view(-1)
         dw = None

@@ -390,3 +390,16 @@ def test_spmm_pull_marked_equals_push(d):
         assert np.array_equal(y1, y2)
     bits, _ = ops._rowset(g)
     assert int(bits.abs().sum()) == 0
+
+
+@pytest.mark.parametrize('d', [64, 20])
+def test_spmm_epilogue_row_scale(d):
+    """y = row_scale[r] * (alpha A x + beta add), fast (d=64) and generic (d=20) kernels, split rows included."""
+    g, v = rand_graph(700, 500, 20000, seed=5, skew=True, split_threshold=64, chunk_edges=64)
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((500, d)).astype(np.float32)
+    add = rng.standard_normal((700, d)).astype(np.float32)
+    rs = rng.uniform(0.1, 2.0, 700).astype(np.float32)
+    y = ops.spmm(g, t(x), t(v), epi=ops.epilogue(alpha=0.5, beta=2.0, add=t(add), row_scale=t(rs)))
+    ref = rs[:, None].astype(np.float64) * (0.5 * O.spmm64(oracle_csr(g, v), x) + 2.0 * add)
+    close(y.cpu().numpy(), ref)

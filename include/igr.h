@@ -183,23 +183,27 @@ int igr_spmm_push_f32(const igr_csr *g, int32_t d, const int64_t *rows, int64_t 
 /* The push without atomics (the training backward uses this one): mark the
  * selected rows, sum repeated rows' sources into one slot each, then every
  * output row gathers only from marked columns:
- *   igr_rowset_mark:  bits[r/32] |= 1 << r%32, slot[r] = some i with rows[i] = r
- *                     (bits zero on entry; bits: uint32[(n+31)/32], slot: int32[n])
+ *   igr_rowset_mark:  bits[r/32] |= 1 << r%32, slot[r] = some i with rows[i] = r,
+ *                     and the same for h = r mod 2^19 in filter (bits, filter zero
+ *                     on entry; bits: uint32[(n+31)/32], filter: uint32[16384],
+ *                     slot: int32[n])
  *   igr_rowset_sum_f32: agg[slot[rows[i]]] += scale * src[i]   (agg zero on entry)
  *   igr_spmm_pull_marked_f32: out[c] = scale * (sum_{p in row c, col[p] marked}
  *                     rhs[p] agg[slot[col[p]]] + self_add [c marked] agg[slot[c]])
  *                     (one lane group per row, fixed order: deterministic
  *                     for distinct rows; repeats are summed into their slot
- *                     with float atomics)
- *   igr_rowset_clear: zero the words of bits holding the selected rows
+ *                     with float atomics).  Persistent 1024-thread workgroups
+ *                     keep the 64 KB filter in LDS; only filter hits probe bits
+ *   igr_rowset_clear: zero the words of bits and filter holding the selected rows
  * On the reverse graph, out = A^T G (+ G): igr_spmm_push_f32's result. */
-int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, int32_t *slot, void *stream);
+int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, int32_t *slot,
+                    void *stream);
 int igr_rowset_sum_f32(int64_t n_sel, int32_t d, const int64_t *rows, const int32_t *slot, const float *src,
                        int64_t lds, float scale, float *agg, int64_t ld_agg, void *stream);
-int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint32_t *bits, const int32_t *slot, const float *agg,
-                             int64_t ld_agg, const float *rhs, float scale, int32_t self_add, float *out, int64_t ldo,
-                             void *stream);
-int igr_rowset_clear(int64_t n_sel, const int64_t *rows, uint32_t *bits, void *stream);
+int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint32_t *bits, const uint32_t *filter,
+                             const int32_t *slot, const float *agg, int64_t ld_agg, const float *rhs, float scale,
+                             int32_t self_add, float *out, int64_t ldo, void *stream);
+int igr_rowset_clear(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, void *stream);
 
 /* The uniforms igr_spmm_scaled_f32 draws for edge ids 0..n-1 (for tests and
  * for an explicit-values replay of the same mask). */

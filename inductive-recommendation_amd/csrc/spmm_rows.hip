@@ -13,6 +13,8 @@
 // edges in 16-edge blocks, so a hub row is spread over the whole workgroup.
 // rows_f32 reduces the groups through LDS in a fixed order (deterministic);
 // push_f32 adds with float atomics (order of adds not fixed).
+#include <algorithm>
+
 #include "common.h"
 
 namespace igr {
@@ -159,18 +161,32 @@ extern "C" int igr_spmm_push_f32(const igr_csr *g, int32_t d, const int64_t *row
 // rows; repeated rows meet in agg through float atomics).
 namespace igr {
 
+// LDS filter of the marked set: bit (r mod 2^19), 64 KB - two 1024-thread
+// workgroups per CU hold it in LDS, so the per-edge probe never leaves the CU;
+// only filter hits (the marked rows plus ~n_sel/2^19 false positives) probe
+// the exact bitmap in L2.
+constexpr int kFilterLog2 = 19;
+constexpr uint32_t kFilterMask = (1u << kFilterLog2) - 1;
+constexpr int kFilterWords = (1 << kFilterLog2) / 32;
+
 __global__ void rowset_mark_kernel(int64_t n, const int64_t *__restrict__ rows, uint32_t *__restrict__ bits,
-                                   int32_t *__restrict__ slot) {
+                                   uint32_t *__restrict__ filter, int32_t *__restrict__ slot) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t r = rows[i];
     atomicOr(bits + (r >> 5), 1u << (r & 31));
+    const uint32_t h = (uint32_t)r & kFilterMask;
+    atomicOr(filter + (h >> 5), 1u << (h & 31));
     slot[r] = (int32_t)i;  // any one of a repeated row's positions
 }
 
-__global__ void rowset_clear_kernel(int64_t n, const int64_t *__restrict__ rows, uint32_t *__restrict__ bits) {
+__global__ void rowset_clear_kernel(int64_t n, const int64_t *__restrict__ rows, uint32_t *__restrict__ bits,
+                                    uint32_t *__restrict__ filter) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) bits[rows[i] >> 5] = 0u;  // every bit set in the word belongs to a selected row
+    if (i >= n) return;
+    const int64_t r = rows[i];
+    bits[r >> 5] = 0u;  // every bit set in these words belongs to a selected row
+    filter[((uint32_t)r & kFilterMask) >> 5] = 0u;
 }
 
 // agg[slot[rows[i]]] += scale * src[i]; agg zero on entry (repeats: float atomics on n_sel x d)
@@ -185,103 +201,116 @@ __global__ void rowset_sum_kernel(int64_t n, int d, const int64_t *__restrict__ 
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void spmm_pull_marked_kernel(
+__global__ __launch_bounds__(1024) void spmm_pull_marked_kernel(
     int64_t n_rows, const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
-    const float *__restrict__ val, const uint32_t *__restrict__ bits, const int32_t *__restrict__ slot,
-    const float *__restrict__ agg, int64_t ld_agg, float *__restrict__ out, int64_t ldo, float scale, int self_add) {
+    const float *__restrict__ val, const uint32_t *__restrict__ bits, const uint32_t *__restrict__ filter,
+    int exact_filter, const int32_t *__restrict__ slot, const float *__restrict__ agg, int64_t ld_agg,
+    float *__restrict__ out, int64_t ldo, float scale, int self_add) {
     constexpr int LPR = D / 4;  // lanes per row, one float4 each
+    constexpr int RPB = 1024 / LPR;  // rows per workgroup pass
+    constexpr int U = 4;  // blocks of LPR edges per trip (independent loads in flight)
+    __shared__ uint32_t sf[kFilterWords];
+    for (int k = threadIdx.x; k < kFilterWords / 4; k += 1024)
+        reinterpret_cast<uint4 *>(sf)[k] = reinterpret_cast<const uint4 *>(filter)[k];
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int sub = lane & (LPR - 1);
     const int gbase = lane - sub;  // first lane of this row's group within the wave
-    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
-    const bool live = r < n_rows;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    int64_t b = 0, e = 0;
-    if (live) {
-        b = row_ptr[r];
-        e = row_ptr[r + 1];
-        if (self_add && ((bits[r >> 5] >> (r & 31)) & 1u))
-            acc = *reinterpret_cast<const float4 *>(agg + (int64_t)slot[r] * ld_agg + sub * 4);
-    }
-    // uniform trip count across the wave (shuffles need every lane)
-    int64_t len = e - b;
-    for (int o = 32; o >= 1; o >>= 1) len = max(len, (int64_t)__shfl_xor((long long)len, o, 64));
-    // U blocks of LPR edges per trip: U independent col loads, then U bitmap
-    // probes in flight per lane (the loop is latency-bound, not byte-bound);
-    // hits are applied in CSR order (block u, then lane j), so the sum order
-    // is fixed.
-    constexpr int U = 4;
     const uint64_t gmask = LPR == 64 ? ~0ull : ((1ull << LPR) - 1);
-    for (int64_t k = 0; k < len; k += LPR * U) {
-        int cu[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t p = b + k + u * LPR + sub;
-            cu[u] = p < e ? col[p] : -1;
+    // persistent: the grid strides over row passes (every wave runs the same trip count)
+    for (int64_t r0 = (int64_t)blockIdx.x * RPB; r0 < n_rows; r0 += (int64_t)gridDim.x * RPB) {
+        const int64_t r = r0 + threadIdx.x / LPR;
+        const bool live = r < n_rows;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        int64_t b = 0, e = 0;
+        if (live) {
+            b = row_ptr[r];
+            e = row_ptr[r + 1];
+            if (self_add && ((bits[r >> 5] >> (r & 31)) & 1u))
+                acc = *reinterpret_cast<const float4 *>(agg + (int64_t)slot[r] * ld_agg + sub * 4);
         }
-        uint32_t wu[U];
+        int64_t len = e - b;  // uniform trip count across the wave (shuffles need every lane)
+        for (int o = 32; o >= 1; o >>= 1) len = max(len, (int64_t)__shfl_xor((long long)len, o, 64));
+        for (int64_t k = 0; k < len; k += LPR * U) {
+            int cu[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) wu[u] = cu[u] >= 0 ? bits[cu[u] >> 5] : 0u;
-        // hit lanes fetch their slot and edge value in parallel (one latency per trip)
-        bool hu[U];
-        int su[U];
-        float vu[U];
+            for (int u = 0; u < U; ++u) {
+                const int64_t p = b + k + u * LPR + sub;
+                cu[u] = p < e ? col[p] : -1;
+            }
+            bool hu[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            hu[u] = cu[u] >= 0 && ((wu[u] >> (cu[u] & 31)) & 1u);
-            su[u] = hu[u] ? slot[cu[u]] : 0;
-            vu[u] = hu[u] ? (val ? val[b + k + u * LPR + sub] : 1.f) : 0.f;
-        }
+            for (int u = 0; u < U; ++u) {
+                const uint32_t h = (uint32_t)cu[u] & kFilterMask;
+                hu[u] = cu[u] >= 0 && ((sf[h >> 5] >> (h & 31)) & 1u);
+            }
+            if (!exact_filter) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            uint64_t hit = (__ballot(hu[u]) >> gbase) & gmask;
-            while (__builtin_amdgcn_readfirstlane((int)(__ballot(hit != 0) != 0))) {
-                // each group walks its own hits two at a time (both agg rows in flight);
-                // groups without hits idle through the loop
-                const int j1 = hit ? __builtin_ctzll(hit) : 0;
-                const uint64_t rest = hit & (hit - 1);
-                const int j2 = rest ? __builtin_ctzll(rest) : j1;
-                const int s1 = __shfl(su[u], gbase + j1, 64), s2 = __shfl(su[u], gbase + j2, 64);
-                const float w1 = __shfl(vu[u], gbase + j1, 64), w2 = __shfl(vu[u], gbase + j2, 64);
-                if (hit) {
-                    const float4 a1 = *reinterpret_cast<const float4 *>(agg + (int64_t)s1 * ld_agg + sub * 4);
-                    if (rest) {
-                        const float4 a2 = *reinterpret_cast<const float4 *>(agg + (int64_t)s2 * ld_agg + sub * 4);
-                        acc = f4_fma(w1, a1, acc);
-                        acc = f4_fma(w2, a2, acc);
-                        hit = rest & (rest - 1);
-                    } else {
-                        acc = f4_fma(w1, a1, acc);
-                        hit = 0;
+                for (int u = 0; u < U; ++u)
+                    if (hu[u]) hu[u] = (bits[cu[u] >> 5] >> (cu[u] & 31)) & 1u;
+            }
+            // hit lanes fetch their slot and edge value in parallel
+            int su[U];
+            float vu[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                su[u] = hu[u] ? slot[cu[u]] : 0;
+                vu[u] = hu[u] ? (val ? val[b + k + u * LPR + sub] : 1.f) : 0.f;
+            }
+            // hits applied in CSR order (block u, then lane j): fixed summation order
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                uint64_t hit = (__ballot(hu[u]) >> gbase) & gmask;
+                while (__builtin_amdgcn_readfirstlane((int)(__ballot(hit != 0) != 0))) {
+                    // each group walks its own hits two at a time (both agg rows in flight)
+                    const int j1 = hit ? __builtin_ctzll(hit) : 0;
+                    const uint64_t rest = hit & (hit - 1);
+                    const int j2 = rest ? __builtin_ctzll(rest) : j1;
+                    const int s1 = __shfl(su[u], gbase + j1, 64), s2 = __shfl(su[u], gbase + j2, 64);
+                    const float w1 = __shfl(vu[u], gbase + j1, 64), w2 = __shfl(vu[u], gbase + j2, 64);
+                    if (hit) {
+                        const float4 a1 = *reinterpret_cast<const float4 *>(agg + (int64_t)s1 * ld_agg + sub * 4);
+                        if (rest) {
+                            const float4 a2 =
+                                *reinterpret_cast<const float4 *>(agg + (int64_t)s2 * ld_agg + sub * 4);
+                            acc = f4_fma(w1, a1, acc);
+                            acc = f4_fma(w2, a2, acc);
+                            hit = rest & (rest - 1);
+                        } else {
+                            acc = f4_fma(w1, a1, acc);
+                            hit = 0;
+                        }
                     }
                 }
             }
         }
+        if (live) *reinterpret_cast<float4 *>(out + r * ldo + sub * 4) = f4_scale(scale, acc);
     }
-    if (live) *reinterpret_cast<float4 *>(out + r * ldo + sub * 4) = f4_scale(scale, acc);
 }
 
 }  // namespace igr
 
 static unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
-extern "C" int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, int32_t *slot, void *stream) {
+extern "C" int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, int32_t *slot,
+                               void *stream) {
     return guarded("igr_rowset_mark", [&]() -> int {
         if (n_sel <= 0) return IGR_OK;
-        if (!rows || !bits || !slot) return arg_error("igr_rowset_mark", "NULL pointer");
+        if (!rows || !bits || !filter || !slot) return arg_error("igr_rowset_mark", "NULL pointer");
         if (n_sel > 2147483647) return arg_error("igr_rowset_mark", "too many rows");
         hipLaunchKernelGGL(rowset_mark_kernel, dim3(blocks_for(n_sel, 256)), dim3(256), 0,
-                           reinterpret_cast<hipStream_t>(stream), n_sel, rows, bits, slot);
+                           reinterpret_cast<hipStream_t>(stream), n_sel, rows, bits, filter, slot);
         return launch_status("igr_rowset_mark");
     });
 }
 
-extern "C" int igr_rowset_clear(int64_t n_sel, const int64_t *rows, uint32_t *bits, void *stream) {
+extern "C" int igr_rowset_clear(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter,
+                                void *stream) {
     return guarded("igr_rowset_clear", [&]() -> int {
         if (n_sel <= 0) return IGR_OK;
-        if (!rows || !bits) return arg_error("igr_rowset_clear", "NULL pointer");
+        if (!rows || !bits || !filter) return arg_error("igr_rowset_clear", "NULL pointer");
         hipLaunchKernelGGL(rowset_clear_kernel, dim3(blocks_for(n_sel, 256)), dim3(256), 0,
-                           reinterpret_cast<hipStream_t>(stream), n_sel, rows, bits);
+                           reinterpret_cast<hipStream_t>(stream), n_sel, rows, bits, filter);
         return launch_status("igr_rowset_clear");
     });
 }
@@ -299,12 +328,12 @@ extern "C" int igr_rowset_sum_f32(int64_t n_sel, int32_t d, const int64_t *rows,
     });
 }
 
-extern "C" int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint32_t *bits, const int32_t *slot,
-                                        const float *agg, int64_t ld_agg, const float *rhs, float scale,
-                                        int32_t self_add, float *out, int64_t ldo, void *stream) {
+extern "C" int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint32_t *bits, const uint32_t *filter,
+                                        const int32_t *slot, const float *agg, int64_t ld_agg, const float *rhs,
+                                        float scale, int32_t self_add, float *out, int64_t ldo, void *stream) {
     return guarded("igr_spmm_pull_marked_f32", [&]() -> int {
         const char *fn = "igr_spmm_pull_marked_f32";
-        if (!g || !bits || !slot) return arg_error(fn, "graph / bits / slot NULL");
+        if (!g || !bits || !filter || !slot) return arg_error(fn, "graph / bits / filter / slot NULL");
         if (g->edge_id && rhs) return arg_error(fn, "rhs by edge id with an edge_id permutation is not supported");
         if (self_add && g->n_rows > g->n_cols) return arg_error(fn, "self_add needs a square graph");
         if (ld_agg < d || ldo < d || ld_agg % 4 || ldo % 4 || !aligned16(agg) || !aligned16(out))
@@ -312,9 +341,21 @@ extern "C" int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint3
         if (g->n_rows <= 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         const int64_t n = g->n_rows;
-#define IGR_PULL(DD)                                                                                         \
-    hipLaunchKernelGGL((spmm_pull_marked_kernel<DD>), dim3(blocks_for(n, 256 / (DD / 4))), dim3(256), 0, st, n, \
-                       g->row_ptr, g->col_idx, rhs, bits, slot, agg, ld_agg, out, ldo, scale, (int)self_add)
+        // the filter is exact when every column index fits in it
+        const int exact = g->n_cols <= (int64_t(1) << kFilterLog2);
+        // persistent grid: two 1024-thread workgroups (2 x 64 KB of filter) per CU
+        static int cus = 0;
+        if (cus <= 0) {
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+                cus = 256;
+        }
+#define IGR_PULL(DD)                                                                                               \
+    hipLaunchKernelGGL((spmm_pull_marked_kernel<DD>),                                                             \
+                       dim3((unsigned)std::min<int64_t>(2 * (int64_t)cus, blocks_for(n, 1024 / (DD / 4)))),       \
+                       dim3(1024), 0, st, n, g->row_ptr, g->col_idx, rhs, bits, filter, exact, slot, agg, ld_agg, \
+                       out, ldo, scale, (int)self_add)
         switch (d) {
             case 32: IGR_PULL(32); break;
             case 64: IGR_PULL(64); break;

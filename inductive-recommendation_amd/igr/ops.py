@@ -515,11 +515,12 @@ def spmm_push(g: Graph, rows, src, dst, rhs=None, scale=1.0, self_add=False):
 
 
 def _rowset(g: Graph):
-    """Per-graph bitmap (zero between uses) + slot map over the column space."""
+    """Per-graph bitmap + 64 KB LDS filter (both zero between uses) + slot map over the column space."""
     rs = getattr(g, '_rowset', None)
     if rs is None:
         n = g.n_cols
         rs = (torch.zeros((n + 31) // 32, dtype=torch.int32, device=g.device),
+              torch.zeros(1 << 14, dtype=torch.int32, device=g.device),
               torch.empty(max(n, 1), dtype=torch.int32, device=g.device))
         g._rowset = rs
     return rs
@@ -535,17 +536,17 @@ def spmm_pull(g: Graph, rows, src, rhs=None, scale=1.0, self_add=False, out=None
     src, lds = _rows(src)
     d = src.shape[1]
     rows = rows.to(torch.int64).contiguous()
-    bits, slot = _rowset(g)
+    bits, filt, slot = _rowset(g)
     agg = torch.zeros(max(rows.numel(), 1), d, dtype=torch.float32, device=src.device)
     if out is None:
         out = torch.empty(g.n_rows, d, dtype=torch.float32, device=src.device)
     st = _stream()
-    L.call('igr_rowset_mark', rows.numel(), _p(rows), _p(bits), _p(slot), st)
+    L.call('igr_rowset_mark', rows.numel(), _p(rows), _p(bits), _p(filt), _p(slot), st)
     L.call('igr_rowset_sum_f32', rows.numel(), d, _p(rows), _p(slot), _p(src), lds, 1.0, _p(agg), agg.stride(0), st)
-    L.call('igr_spmm_pull_marked_f32', ctypes.byref(g.csr), d, _p(bits), _p(slot), _p(agg), agg.stride(0),
+    L.call('igr_spmm_pull_marked_f32', ctypes.byref(g.csr), d, _p(bits), _p(filt), _p(slot), _p(agg), agg.stride(0),
            _p(None if rhs is None else _f32(rhs).contiguous()), float(scale), int(bool(self_add)), _p(out),
            out.stride(0), st)
-    L.call('igr_rowset_clear', rows.numel(), _p(rows), _p(bits), st)
+    L.call('igr_rowset_clear', rows.numel(), _p(rows), _p(bits), _p(filt), st)
     return out
 
 

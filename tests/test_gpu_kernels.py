@@ -388,8 +388,8 @@ def test_spmm_pull_marked_equals_push(d):
         y1 = ops.spmm_pull(g, t(u), t(src[:len(u)]), t(vv), scale=0.5, self_add=True).cpu().numpy()
         y2 = ops.spmm_pull(g, t(u), t(src[:len(u)]), t(vv), scale=0.5, self_add=True).cpu().numpy()
         assert np.array_equal(y1, y2)
-    bits, _ = ops._rowset(g)
-    assert int(bits.abs().sum()) == 0
+    bits, filt, _ = ops._rowset(g)
+    assert int(bits.abs().sum()) == 0 and int(filt.abs().sum()) == 0
 
 
 @pytest.mark.parametrize('d', [64, 20])
@@ -403,3 +403,32 @@ def test_spmm_epilogue_row_scale(d):
     y = ops.spmm(g, t(x), t(v), epi=ops.epilogue(alpha=0.5, beta=2.0, add=t(add), row_scale=t(rs)))
     ref = rs[:, None].astype(np.float64) * (0.5 * O.spmm64(oracle_csr(g, v), x) + 2.0 * add)
     close(y.cpu().numpy(), ref)
+
+
+def test_spmm_pull_filter_collisions_large_graph():
+    """n > 2^19: the LDS filter is not exact; columns r + 2^19 collide with marked
+    rows r in the filter and must be rejected by the exact bitmap."""
+    n, d = 700_000, 64
+    rng = np.random.default_rng(3)
+    rows = rng.integers(0, n - (1 << 19), 500)
+    rows = np.concatenate([rows, rows[:50] + (1 << 19) - 1])  # some marked rows above 2^19 too
+    a = np.concatenate([rng.integers(0, n, 150_000), rng.integers(0, n, 5000)])
+    b = np.concatenate([rng.integers(0, n, 150_000), rows[rng.integers(0, 500, 5000)] + (1 << 19)])  # colliders
+    b[-5000:] = np.minimum(b[-5000:], n - 1)
+    c = np.concatenate([a[:2000], rows[:2000 % 550]])  # edges into marked rows
+    a2 = np.concatenate([a, rng.integers(0, n, len(c))])
+    b2 = np.concatenate([b, c])
+    v = rng.standard_normal(len(a2)).astype(np.float32)
+    g, vv = G.Graph.from_coo(np.concatenate([a2, b2]), np.concatenate([b2, a2]), n, n, np.concatenate([v, v]),
+                             dedup=True, device=DEV, symmetric=True)
+    src = rng.standard_normal((len(rows), d)).astype(np.float32)
+    y = ops.spmm_pull(g, t(rows), t(src), t(vv), self_add=True).cpu().numpy()
+    h = g.host()
+    S = np.zeros((n, d))
+    np.add.at(S, rows, src.astype(np.float64))
+    erow = np.repeat(np.arange(n), np.diff(h['row_ptr']))
+    ref = S.copy()
+    np.add.at(ref, h['col_idx'], vv.astype(np.float64)[:, None] * S[erow])
+    close(y, ref, atol_row=2e-6)
+    bits, filt, _ = ops._rowset(g)
+    assert int(bits.abs().sum()) == 0 and int(filt.abs().sum()) == 0

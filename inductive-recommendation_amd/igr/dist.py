@@ -139,12 +139,18 @@ class BipartiteShard:
         out.append(('user', self.user_block, 'items', self.user_block.n_rows, self.user_block.nnz))
         return out
 
-    def layer(self, x_users, x_items, y_users=None, y_items=None, group=None, spmm=None, hook=None):
+    def layer(self, x_users, x_items, y_users=None, y_items=None, group=None, spmm=None, hook=None,
+              add_users=None, add_items=None, beta=0.0, pending=()):
         """One layer: returns (Y[U_k], Y[I]) with Y[I] all-reduced across ranks.
 
-        `spmm(g, x, vals, out, accumulate)` defaults to the HIP kernel (the CPU
-        gloo tests pass the oracle); `hook(i, 'start'|'end')` brackets each
-        SpMM launch (bench timing)."""
+        With add_users / add_items: Y[U_k] += beta * add_users and every rank
+        adds beta * add_items (its own item terms) to its partial before the
+        reduce - the training backward's "+ g/(L+1)" (dist_train.py).
+        `pending`: collectives producing x_items, waited for just before the
+        user-side SpMM (the item side needs only x_users).
+        `spmm(g, x, vals, out, accumulate, add=None, beta=0.)` defaults to the
+        HIP kernel (the CPU gloo tests pass the oracle); `hook(i, 'start'|'end')`
+        brackets each SpMM launch (bench timing)."""
         hook = hook or (lambda i, ph: None)
         spmm = spmm or _hip_spmm
         if y_items is None:
@@ -154,20 +160,33 @@ class BipartiteShard:
             yk = y_items[r0:r1]
             for t, (g, v, c0, c1) in enumerate(tiles):
                 hook(i, 'start')
-                spmm(g, x_users[c0:c1], v, yk, t > 0)
+                if t == 0 and add_items is not None:
+                    spmm(g, x_users[c0:c1], v, yk, False, add=add_items[r0:r1], beta=beta)
+                else:
+                    spmm(g, x_users[c0:c1], v, yk, t > 0)
                 hook(i, 'end')
                 i += 1
             if self.world > 1:
                 works.append(dist.all_reduce(yk, op=dist.ReduceOp.SUM, group=group, async_op=True))
         if y_users is None:
             y_users = torch.empty(self.u1 - self.u0, x_items.shape[1], dtype=torch.float32, device=x_items.device)
+        for w in pending:
+            w.wait()
         hook(i, 'start')
-        spmm(self.user_block, x_items, self.user_vals, y_users, False)
+        if add_users is not None:
+            spmm(self.user_block, x_items, self.user_vals, y_users, False, add=add_users, beta=beta)
+        else:
+            spmm(self.user_block, x_items, self.user_vals, y_users, False)
         hook(i, 'end')
         for w in works:
             w.wait()
         return y_users, y_items
 
 
-def _hip_spmm(g, x, vals, out, accumulate):
-    return ops.spmm(g, x, vals, out=out, epi=ops.epilogue(beta=1.0, add=out) if accumulate else None)
+def _hip_spmm(g, x, vals, out, accumulate, add=None, beta=0.0):
+    """out = A x (+ out if accumulate) (+ beta * add), through the SpMM epilogue."""
+    if accumulate:
+        return ops.spmm(g, x, vals, out=out, epi=ops.epilogue(beta=1.0, add=out))
+    if add is not None:
+        return ops.spmm(g, x, vals, out=out, epi=ops.epilogue(beta=beta, add=add))
+    return ops.spmm(g, x, vals, out=out)

@@ -1,0 +1,280 @@
+"""igr.dist_train - IGCN training sharded across the GPUs of a node ("Training").
+
+The reference trains on one device (trainer.py:518-561); this is the build's
+data-parallel restatement of the same step over the partition of igr.dist:
+
+  * rank k owns the users U_k = [u0, u1) (edge-balanced ranges), their rows of
+    the adjacency (both directions) and their user FEATURES; the item
+    features and the two general features are replicated;
+  * the rank's embedding table is E_k = [E[U_k]; E[items]; E[gen_u]; E[gen_i]]
+    (feature_ratio = 1: user u's feature is u, item i's is U + i,
+    IGCN.generate_feat / model.py:4139-4175);
+  * one feature graph per rank, rows [local users; items] x columns E_k: a
+    user row reads its items' features and gen_u; an item row reads its local
+    users' features (+ gen_i on rank 0 only), so its output is a partial sum.
+
+Forward (IGCN.get_rep, model.py:4188-4200):
+  x0 = F_k E_k                               item rows all-reduced (async,
+                                             overlapping layer 1's item side)
+  x_{l+1} = A x_l                            BipartiteShard.layer: one item
+                                             all-reduce per layer
+  rep_k = [mean_l x_l[U_k]; mean_l x_l[I]]   items identical on every rank
+Backward (A symmetric, so the same blocks):
+  dX_L  = g / (L+1), item part all-reduced once (every rank's batch items)
+  dX_l  = A dX_{l+1} + g / (L+1)             each rank folds its own item terms
+                                             into its partial before the reduce
+  dE_k  = F_k^T dX_0                         owned user-feature rows complete;
+                                             replicated rows partial
+Step (IGCNTrainer.step, trainer.py:531-561): every rank samples its batch
+from its own users (device sampler), loss_k = (bpr + l2_reg l2 + aux_reg aux)
+/ world, backward, ONE all-reduce of the replicated rows' gradients and w's
+(DDP-style), fused Adam on every rank (identical replicated updates).  The
+global step is a batch of world x B samples (weak scaling, as DDP).
+
+The SpMM is pluggable (`spmm=`) so the CPU gloo tests run the same code with
+the oracle; on a GPU it is the HIP kernel.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import ops
+from .dist import BipartiteShard, _hip_spmm
+from .graph import Graph, csr_from_coo
+from .model import train_pairs
+
+
+def _allreduce(t, group, async_op=False):
+    return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+
+
+class FeatureShard:
+    """The rank's rows of IGCN's feature graph over its embedding table E_k.
+
+    Rows [0, n_k) are the local users, rows n_k + i the items; columns index
+    E_k: local user features [0, n_k), item features n_k + i, gen_u at
+    n_k + I, gen_i at n_k + I + 1.  row_sum is the GLOBAL row sum of the
+    reference's feature matrix (duplicates counted, + 1 for the general
+    feature), so the values equal the unsharded model's."""
+
+    def __init__(self, pairs, n_users, n_items, u0, u1, rank, device):
+        U, I = n_users, n_items
+        nk = u1 - u0
+        u, i = pairs[:, 0], pairs[:, 1]
+        mine = (u >= u0) & (u < u1)
+        lu, li = u[mine] - u0, i[mine]
+        rows = [lu, nk + li, np.arange(nk)]
+        cols = [nk + li, lu, np.full(nk, nk + I)]
+        if rank == 0:  # the general item feature enters the item rows' sum once
+            rows.append(nk + np.arange(I))
+            cols.append(np.full(I, nk + I + 1))
+        rp, ci, _, _ = csr_from_coo(np.concatenate(rows), np.concatenate(cols), nk + I, nk + I + 2, None,
+                                    dedup=True, want_eid=False)
+        self.graph = Graph(rp, ci, nk + I, nk + I + 2, device=device)
+        deg_u = np.bincount(u, minlength=U).astype(np.float32)
+        deg_i = np.bincount(i, minlength=I).astype(np.float32)
+        self.row_sum = torch.from_numpy(np.concatenate([deg_u[u0:u1], deg_i]) + np.float32(1.)).to(device)
+        self.n_local, self.n_items = nk, I
+
+    def row_values(self, alpha):
+        """Per-row value row_sum ** ((alpha - 1)/2 - 0.5) (IGCN.update_feat_mat, model.py:4127-4130)."""
+        ex = (alpha - 1.) / 2. - 0.5
+        return self.row_sum.double().pow(ex).float() if not self.row_sum.is_cuda else \
+            ops.feat_row_values(self.row_sum, ex)
+
+    def edge_values(self, alpha):
+        """The same values per edge (CPU / explicit path)."""
+        rv = self.row_values(alpha)
+        h = self.graph.host()
+        rows = torch.from_numpy(np.repeat(np.arange(self.graph.n_rows), np.diff(h['row_ptr']))).to(rv.device)
+        return rv[rows].contiguous()
+
+
+class ShardedPropagate(torch.autograd.Function):
+    """rep_k = [rep[U_k]; rep[I]] of IGCN.get_rep on the rank's shard (see module doc)."""
+
+    @staticmethod
+    def forward(ctx, emb, model, fvals):
+        sh, fs, L, spmm, group = model.shard, model.feat, model.n_layers, model.spmm, model.group
+        ctx.model, ctx.fvals = model, fvals
+        nk = fs.n_local
+        d = emb.shape[1]
+        x0 = torch.empty(nk + fs.n_items, d, dtype=torch.float32, device=emb.device)
+        model.feat_spmm(fs.graph, emb, fvals, x0)
+        xu, xi = x0[:nk], x0[nk:]
+        pend = [_allreduce(xi, group, async_op=True)] if model.world > 1 else []
+        acc = None
+        for _ in range(L):
+            yu, yi = sh.layer(xu, xi, group=group, spmm=spmm, pending=pend)
+            if acc is None:  # x0's item rows are complete once the first layer has waited
+                acc = x0.clone()
+            pend = []
+            acc[:nk].add_(yu)
+            acc[nk:].add_(yi)
+            xu, xi = yu, yi
+        if acc is None:
+            for w in pend:
+                w.wait()
+            acc = x0
+        return acc.div_(float(L + 1))
+
+    @staticmethod
+    def backward(ctx, g):
+        model, fvals = ctx.model, ctx.fvals
+        sh, fs, L, spmm, group = model.shard, model.feat, model.n_layers, model.spmm, model.group
+        nk = fs.n_local
+        L1 = float(L + 1)
+        g = g.contiguous()
+        gu, gi = g[:nk], g[nk:]
+        dxi = gi.clone()
+        if model.world > 1:
+            _allreduce(dxi, group)  # every rank's batch items
+        dxu = gu / L1
+        dxi.div_(L1)
+        for _ in range(L):
+            dxu, dxi = sh.layer(dxu, dxi, group=group, spmm=spmm, add_users=gu, add_items=gi, beta=1.0 / L1)
+        dx0 = torch.cat([dxu, dxi])
+        demb = torch.empty(fs.graph.n_cols, g.shape[1], dtype=torch.float32, device=g.device)
+        model.feat_spmm(fs.graph.reverse(), dx0, fvals, demb, reverse=True)
+        return demb, None, None
+
+
+class ShardedIGCN(nn.Module):
+    """IGCN (model.py:4107-4220) on one rank's shard; feature_ratio = 1."""
+
+    def __init__(self, model_config, rank, world, group=None, spmm=None):
+        super().__init__()
+        ds = model_config['dataset']
+        if model_config.get('feature_ratio', 1.) != 1.:
+            raise ValueError('ShardedIGCN supports feature_ratio = 1 (every node has its own feature)')
+        self.config = model_config
+        self.name = 'IGCN'
+        self.device = model_config['device']
+        self.n_users, self.n_items = ds.n_users, ds.n_items
+        self.embedding_size = d = model_config['embedding_size']
+        self.n_layers = model_config['n_layers']
+        self.dropout = model_config['dropout']
+        self.alpha, self.delta = 1., model_config.get('delta', 0.99)
+        self.rank, self.world, self.group = rank, world, group
+        self.spmm = spmm or _hip_spmm
+        self.hip = spmm is None
+        pairs = train_pairs(ds)
+        self.shard = BipartiteShard(pairs, self.n_users, self.n_items, rank, world, self.device, d=d)
+        self.u0, self.u1 = self.shard.u0, self.shard.u1
+        self.feat = FeatureShard(pairs, self.n_users, self.n_items, self.u0, self.u1, rank, self.device)
+        self.n_local = self.u1 - self.u0
+        self.embedding = nn.Embedding(self.feat.graph.n_cols, d)
+        nn.init.normal_(self.embedding.weight, std=0.1)  # model.py:4124
+        self.w = nn.Parameter(torch.ones([d], dtype=torch.float32, device=self.device))
+        self.to(device=self.device)
+        self.update_feat_mat()
+        self._drop_step = -1
+        self._drop_seed = int(model_config.get('seed', 0)) & (2 ** 63 - 1)
+
+    # ---------------------------------------------------------------- parameters
+    def load_full_embedding(self, full):
+        """Take this rank's rows of an unsharded (U + I + 2) x d table (same layout as IGCN's)."""
+        U = self.n_users
+        with torch.no_grad():
+            self.embedding.weight.copy_(torch.cat([full[self.u0:self.u1], full[U:]]).to(self.device))
+
+    def replicated_rows(self):
+        return slice(self.n_local, self.feat.graph.n_cols)
+
+    def update_feat_mat(self):
+        self.feat_base = self.feat.row_values(self.alpha)
+        self._edge_vals = None
+
+    def feat_mat_anneal(self):
+        self.alpha *= self.delta
+        self.update_feat_mat()
+
+    def feat_values(self):
+        """ScaledWeights on the GPU (dropout drawn in the SpMM with a rank-distinct
+        key: every rank's edges are distinct edges); explicit values otherwise."""
+        if not self.hip:
+            if self.training and self.dropout > 0:
+                raise NotImplementedError('the CPU restatement path runs without dropout')
+            if self._edge_vals is None:
+                self._edge_vals = self.feat.edge_values(self.alpha)
+            return self._edge_vals
+        if self.training and self.dropout > 0:
+            self._drop_step += 1
+            seed = (self._drop_seed * 0x9E3779B97F4A7C15 + self.rank + 1) & (2 ** 63 - 1)
+            return ops.ScaledWeights(self.feat_base, None, 1.0 - self.dropout, seed, self._drop_step)
+        return ops.ScaledWeights(self.feat_base)
+
+    def feat_spmm(self, g, x, fvals, out, reverse=False):
+        if isinstance(fvals, ops.ScaledWeights):
+            return ops.spmm_scaled(g, x, fvals.transposed() if reverse else fvals, out=out)
+        return self.spmm(g, x, fvals, out, False)
+
+    # ---------------------------------------------------------------- model surface
+    def get_rep(self):
+        """[rep[U_k]; rep[I]] (rows of IGCN.get_rep owned / replicated here)."""
+        return ShardedPropagate.apply(self.embedding.weight, self, self.feat_values())
+
+    def bpr_aux_loss(self, users, pos_items, neg_items, a_users, a_pos, a_neg):
+        """IGCNTrainer terms on the local batch (users are LOCAL ids)."""
+        rep = self.get_rep()
+        bpr, l2 = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_local)
+        aux, _ = ops.bpr_loss(self.embedding.weight, a_users, a_pos, a_neg, 0, self.n_local, w=self.w)
+        return bpr, l2, aux
+
+    def sync_grads(self):
+        """One all-reduce of the replicated parameters' gradients (item / general rows and w)."""
+        if self.world == 1:
+            return
+        if self.w.grad is None:
+            self.w.grad = torch.zeros_like(self.w)
+        ge = self.embedding.weight.grad[self.replicated_rows()]
+        buf = torch.cat([ge.reshape(-1), self.w.grad.reshape(-1)])
+        _allreduce(buf, self.group)
+        ge.copy_(buf[:ge.numel()].view_as(ge))
+        self.w.grad.copy_(buf[ge.numel():])
+
+
+class _LocalPairs:
+    """The rank's users' training pairs with local user ids (for the device sampler)."""
+
+    def __init__(self, pairs, u0, u1, n_items):
+        mine = (pairs[:, 0] >= u0) & (pairs[:, 0] < u1)
+        p = pairs[mine].copy()
+        p[:, 0] -= u0
+        self.train_pairs, self.n_users, self.n_items = p, u1 - u0, n_items
+
+    def __len__(self):
+        return len(self.train_pairs)
+
+
+class ShardedIGCNTrainer:
+    """IGCNTrainer.step (trainer.py:531-561) on every rank of a sharded model."""
+
+    def __init__(self, trainer_config, model):
+        from .optim import Adam
+        from .sampler import DeviceBPRSampler
+        self.model = model
+        self.config = trainer_config
+        self.batch_size = trainer_config['batch_size']
+        self.l2_reg, self.aux_reg = trainer_config['l2_reg'], trainer_config['aux_reg']
+        seed = int(trainer_config.get('seed', 0))
+        local = _LocalPairs(train_pairs(model.config['dataset']), model.u0, model.u1, model.n_items)
+        # aux pairs = the dataset itself at feature_ratio = 1 (AuxiliaryDataset), local user ids
+        self.sampler = DeviceBPRSampler(local, self.batch_size, model.device, seed=seed * 1000003 + model.rank)
+        self.aux_sampler = DeviceBPRSampler(local, self.batch_size, model.device,
+                                            seed=(seed + 1) * 1000003 + model.rank)
+        self.opt = Adam(model.parameters(), lr=trainer_config['lr'])
+
+    def step(self, users=None, pos=None, neg=None, a_users=None, a_pos=None, a_neg=None):
+        m = self.model
+        if users is None:
+            users, pos, neg = self.sampler.sample(self.batch_size)
+            a_users, a_pos, a_neg = self.aux_sampler.sample(self.batch_size)
+        bpr, l2, aux = m.bpr_aux_loss(users, pos, neg, a_users, a_pos, a_neg)
+        loss = bpr + self.l2_reg * l2 + self.aux_reg * aux
+        self.opt.zero_grad()
+        (loss / m.world).backward()
+        m.sync_grads()
+        self.opt.step()
+        return loss

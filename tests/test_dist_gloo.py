@@ -16,14 +16,19 @@ from igr.dist import BipartiteShard, balanced_ranges
 from oracle import igr_oracle as O
 
 
-def oracle_spmm(g, x, vals, out, accumulate):
+def oracle_spmm(g, x, vals, out, accumulate, add=None, beta=0.0):
+    """The rank-local SpMM restated on the CPU: out = A x (+ out) (+ beta add).
+    vals are by edge id (a reverse graph carries the forward edge ids)."""
     h = g.host()
-    A = O.CSR(g.n_rows, g.n_cols, h['row_ptr'], h['col_idx'].astype(np.int64), vals.numpy())
+    v = vals.numpy() if h['edge_id'] is None else vals.numpy()[h['edge_id']]
+    A = O.CSR(g.n_rows, g.n_cols, h['row_ptr'], h['col_idx'].astype(np.int64), v)
     y = torch.from_numpy(O.spmm(A, np.ascontiguousarray(x.numpy())))
     if accumulate:
         out.add_(y)
     else:
         out.copy_(y)
+    if add is not None:
+        out.add_(beta * add)
     return out
 
 
@@ -103,3 +108,79 @@ def test_item_chunks_identical_across_ranks():
     cuts = [[(r0, r1) for r0, r1, _ in BipartiteShard(pairs, U, I, r, 4, 'cpu').chunks] for r in range(4)]
     assert all(c == cuts[0] for c in cuts) and len(cuts[0]) == 4
     assert cuts[0][0][0] == 0 and cuts[0][-1][1] == I
+
+
+# ------------------------------------------------------------------ sharded IGCN training (dist_train.py)
+
+class _DS:
+    def __init__(self, pairs, U, I):
+        self.train_pairs, self.n_users, self.n_items = pairs, U, I
+        self.name = 'synthetic'
+
+    def __len__(self):
+        return len(self.train_pairs)
+
+
+def _igcn_worker(rank, world, port, pairs, U, I, d, L, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from igr.dist_train import ShardedIGCN
+        m = ShardedIGCN({'dataset': _DS(pairs, U, I), 'embedding_size': d, 'n_layers': L, 'dropout': 0.3,
+                         'device': 'cpu', 'feature_ratio': 1.}, rank, world, spmm=oracle_spmm)
+        m.eval()  # no dropout on the CPU restatement path
+        g = torch.Generator().manual_seed(0)
+        emb = torch.randn(U + I + 2, d, generator=g) * 0.1
+        R = torch.randn(U + I, d, generator=g)
+        m.load_full_embedding(emb)
+        rep = m.get_rep()
+        G = torch.cat([R[m.u0:m.u1], R[U:] * (rank + 1)])  # rank-specific item terms: they must be summed
+        (rep * G).sum().backward()
+        m.sync_grads()
+        q.put((rank, m.u0, m.u1, rep.detach().numpy(), m.embedding.weight.grad.numpy()))
+    except Exception:
+        import traceback
+        q.put((rank, 'error', traceback.format_exc()))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('L', [0, 2])
+def test_sharded_igcn_rep_and_grad_match_unsharded(L):
+    """World 2: the sharded forward (feature layer + L layers, item all-reduces)
+    and backward (item terms of every rank folded into the reduces, replicated
+    gradients all-reduced) equal the unsharded IGCN restatement."""
+    rng = np.random.default_rng(4)
+    U, I, d = 90, 50, 8
+    pairs = np.stack([rng.integers(0, U, 900), rng.integers(0, I, 900)], 1)
+    pairs = np.concatenate([pairs, pairs[:20]])  # duplicates
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_igcn_worker, args=(r, world, port, pairs, U, I, d, L, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != 'error', r[2]
+    A = O.norm_adj(U, I, pairs)
+    F = O.generate_feat(U, I, pairs)
+    fv = O.feat_values(F, 1.0)
+    g = torch.Generator().manual_seed(0)
+    emb = (torch.randn(U + I + 2, d, generator=g) * 0.1).numpy()
+    R = torch.randn(U + I, d, generator=g).numpy()
+    rep = O.igcn_rep(A, F, fv, emb, L)
+    Gt = np.concatenate([R[:U], R[U:] * sum(k + 1 for k in range(world))])
+    grad = O.igcn_grad(A, F, fv, L, Gt)
+    tol = dict(rtol=1e-5, atol=1e-6)
+    for rank, u0, u1, rep_k, grad_k in res:
+        nk = u1 - u0
+        np.testing.assert_allclose(rep_k[:nk], rep[u0:u1], **tol)
+        np.testing.assert_allclose(rep_k[nk:], rep[U:], **tol)
+        np.testing.assert_allclose(grad_k[:nk], grad[u0:u1], **tol)
+        np.testing.assert_allclose(grad_k[nk:], grad[U:], **tol)

@@ -140,14 +140,16 @@ class BipartiteShard:
         return out
 
     def layer(self, x_users, x_items, y_users=None, y_items=None, group=None, spmm=None, hook=None,
-              add_users=None, add_items=None, beta=0.0, pending=()):
+              add_users=None, add_items=None, beta=0.0, pending=(), acc_users=None, acc_div=1.0):
         """One layer: returns (Y[U_k], Y[I]) with Y[I] all-reduced across ranks.
 
         With add_users / add_items: Y[U_k] += beta * add_users and every rank
         adds beta * add_items (its own item terms) to its partial before the
         reduce - the training backward's "+ g/(L+1)" (dist_train.py).
         `pending`: collectives producing x_items, waited for just before the
-        user-side SpMM (the item side needs only x_users).
+        user-side SpMM (the item side needs only x_users).  acc_users: the
+        user-side epilogue also does acc_users = (acc_users + Y[U_k]) / acc_div
+        (the forward's running layer mean).
         `spmm(g, x, vals, out, accumulate, add=None, beta=0.)` defaults to the
         HIP kernel (the CPU gloo tests pass the oracle); `hook(i, 'start'|'end')`
         brackets each SpMM launch (bench timing)."""
@@ -173,20 +175,23 @@ class BipartiteShard:
         for w in pending:
             w.wait()
         hook(i, 'start')
+        kw = {} if acc_users is None else dict(acc=acc_users, acc_mode=2, acc_div=acc_div)
         if add_users is not None:
-            spmm(self.user_block, x_items, self.user_vals, y_users, False, add=add_users, beta=beta)
+            spmm(self.user_block, x_items, self.user_vals, y_users, False, add=add_users, beta=beta, **kw)
         else:
-            spmm(self.user_block, x_items, self.user_vals, y_users, False)
+            spmm(self.user_block, x_items, self.user_vals, y_users, False, **kw)
         hook(i, 'end')
         for w in works:
             w.wait()
         return y_users, y_items
 
 
-def _hip_spmm(g, x, vals, out, accumulate, add=None, beta=0.0):
-    """out = A x (+ out if accumulate) (+ beta * add), through the SpMM epilogue."""
+def _hip_spmm(g, x, vals, out, accumulate, add=None, beta=0.0, acc=None, acc_mode=0, acc_div=1.0):
+    """out = A x (+ out if accumulate) (+ beta * add), and acc = out (mode 1) or
+    acc = (acc + out) / acc_div (mode 2), all in the SpMM epilogue."""
     if accumulate:
-        return ops.spmm(g, x, vals, out=out, epi=ops.epilogue(beta=1.0, add=out))
-    if add is not None:
-        return ops.spmm(g, x, vals, out=out, epi=ops.epilogue(beta=beta, add=add))
-    return ops.spmm(g, x, vals, out=out)
+        add, beta = out, 1.0
+    if add is None and acc is None:
+        return ops.spmm(g, x, vals, out=out)
+    return ops.spmm(g, x, vals, out=out, epi=ops.epilogue(beta=beta, add=add, acc=acc, acc_mode=acc_mode,
+                                                          acc_div=acc_div))

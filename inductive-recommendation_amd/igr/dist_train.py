@@ -92,52 +92,87 @@ class FeatureShard:
 
 
 class ShardedPropagate(torch.autograd.Function):
-    """rep_k = [rep[U_k]; rep[I]] of IGCN.get_rep on the rank's shard (see module doc)."""
+    """rep_k = [rep[U_k]; rep[I]] of IGCN.get_rep on the rank's shard (see module doc).
+
+    The user rows' running layer mean is kept by the SpMM epilogue (the last
+    layer divides by L+1); the item rows (I x d, complete only after their
+    reduce) are accumulated after it.  aux = (users, pos, neg) (local user
+    ids) also returns the aux BPR term on E_k with w, its gradient added into
+    dE_k in place (as ops.PropagateRows)."""
 
     @staticmethod
-    def forward(ctx, emb, model, fvals):
+    def forward(ctx, emb, w, model, fvals, aux):
         sh, fs, L, spmm, group = model.shard, model.feat, model.n_layers, model.spmm, model.group
-        ctx.model, ctx.fvals = model, fvals
+        ctx.model, ctx.fvals, ctx.aux = model, fvals, aux
+        ctx.save_for_backward(emb if aux is not None else None, w)
         nk = fs.n_local
         d = emb.shape[1]
+        L1 = float(L + 1)
         x0 = torch.empty(nk + fs.n_items, d, dtype=torch.float32, device=emb.device)
-        model.feat_spmm(fs.graph, emb, fvals, x0)
-        xu, xi = x0[:nk], x0[nk:]
+        acc = torch.empty_like(x0)
+        model.feat_spmm(fs.graph, emb, fvals, x0, acc=acc)  # acc = x0 (item rows partial until reduced)
+        xi = x0[nk:]
         pend = [_allreduce(xi, group, async_op=True)] if model.world > 1 else []
-        acc = None
-        for _ in range(L):
-            yu, yi = sh.layer(xu, xi, group=group, spmm=spmm, pending=pend)
-            if acc is None:  # x0's item rows are complete once the first layer has waited
-                acc = x0.clone()
+        bufs = [torch.empty_like(x0), torch.empty_like(x0)]
+        x = x0
+        for layer in range(L):
+            y = bufs[layer % 2]
+            last = layer == L - 1
+            sh.layer(x[:nk], x[nk:], y_users=y[:nk], y_items=y[nk:], group=group, spmm=spmm, pending=pend,
+                     acc_users=acc[:nk], acc_div=L1 if last else 1.0)
+            if layer == 0:
+                acc[nk:].copy_(xi)  # x0's item rows are complete once the first layer has waited
             pend = []
-            acc[:nk].add_(yu)
-            acc[nk:].add_(yi)
-            xu, xi = yu, yi
-        if acc is None:
-            for w in pend:
-                w.wait()
-            acc = x0
-        return acc.div_(float(L + 1))
+            acc[nk:].add_(y[nk:])
+            x = y
+        for wk in pend:
+            wk.wait()
+        if L == 0:
+            acc[nk:].copy_(xi)
+        else:
+            acc[nk:].div_(L1)
+        aux_loss = None
+        if aux is not None:
+            au, ap, an = aux
+            loss = torch.empty(au.numel(), dtype=torch.float32, device=emb.device)
+            ops.L.call('igr_bpr_fwd_bwd_f32', au.numel(), d, ops._p(au), ops._p(ap), ops._p(an), 0, nk,
+                       ops._p(emb), emb.stride(0), ops._p(w), ops._p(loss), None, 0.0, 0.0, None, None, None, 0,
+                       None, ops._stream())
+            aux_loss = loss.mean()
+        return (acc, aux_loss) if aux is not None else acc
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, g_aux=None):
         model, fvals = ctx.model, ctx.fvals
+        emb, w = ctx.saved_tensors
         sh, fs, L, spmm, group = model.shard, model.feat, model.n_layers, model.spmm, model.group
         nk = fs.n_local
         L1 = float(L + 1)
         g = g.contiguous()
         gu, gi = g[:nk], g[nk:]
-        dxi = gi.clone()
+        x = torch.empty_like(g)
+        x[nk:].copy_(gi)
         if model.world > 1:
-            _allreduce(dxi, group)  # every rank's batch items
-        dxu = gu / L1
-        dxi.div_(L1)
-        for _ in range(L):
-            dxu, dxi = sh.layer(dxu, dxi, group=group, spmm=spmm, add_users=gu, add_items=gi, beta=1.0 / L1)
-        dx0 = torch.cat([dxu, dxi])
+            _allreduce(x[nk:], group)  # every rank's batch items
+        torch.div(gu, L1, out=x[:nk])
+        x[nk:].div_(L1)
+        bufs = [torch.empty_like(g), x]
+        for layer in range(L):
+            y = bufs[layer % 2]
+            sh.layer(x[:nk], x[nk:], y_users=y[:nk], y_items=y[nk:], group=group, spmm=spmm, add_users=gu,
+                     add_items=gi, beta=1.0 / L1)
+            x = y
         demb = torch.empty(fs.graph.n_cols, g.shape[1], dtype=torch.float32, device=g.device)
-        model.feat_spmm(fs.graph.reverse(), dx0, fvals, demb, reverse=True)
-        return demb, None, None
+        model.feat_spmm(fs.graph.reverse(), x, fvals, demb, reverse=True)
+        dw = None
+        if ctx.aux is not None and g_aux is not None:
+            au, ap, an = ctx.aux
+            dw = torch.zeros_like(w)
+            g_aux = g_aux.float().contiguous()
+            ops.L.call('igr_bpr_fwd_bwd_f32', au.numel(), emb.shape[1], ops._p(au), ops._p(ap), ops._p(an), 0, nk,
+                       ops._p(emb), emb.stride(0), ops._p(w), None, None, 1.0 / au.numel(), 0.0, ops._p(g_aux),
+                       None, ops._p(demb), demb.stride(0), ops._p(dw), ops._stream())
+        return demb, dw, None, None, None
 
 
 class ShardedIGCN(nn.Module):
@@ -205,21 +240,26 @@ class ShardedIGCN(nn.Module):
             return ops.ScaledWeights(self.feat_base, None, 1.0 - self.dropout, seed, self._drop_step)
         return ops.ScaledWeights(self.feat_base)
 
-    def feat_spmm(self, g, x, fvals, out, reverse=False):
+    def feat_spmm(self, g, x, fvals, out, reverse=False, acc=None):
+        """out = F_w x (reverse: F_w^T x); acc = out via the epilogue when given."""
         if isinstance(fvals, ops.ScaledWeights):
-            return ops.spmm_scaled(g, x, fvals.transposed() if reverse else fvals, out=out)
-        return self.spmm(g, x, fvals, out, False)
+            epi = None if acc is None else ops.epilogue(acc=acc, acc_mode=1)
+            return ops.spmm_scaled(g, x, fvals.transposed() if reverse else fvals, out=out, epi=epi)
+        if acc is None:
+            return self.spmm(g, x, fvals, out, False)
+        return self.spmm(g, x, fvals, out, False, acc=acc, acc_mode=1)
 
     # ---------------------------------------------------------------- model surface
     def get_rep(self):
         """[rep[U_k]; rep[I]] (rows of IGCN.get_rep owned / replicated here)."""
-        return ShardedPropagate.apply(self.embedding.weight, self, self.feat_values())
+        return ShardedPropagate.apply(self.embedding.weight, self.w, self, self.feat_values(), None)
 
     def bpr_aux_loss(self, users, pos_items, neg_items, a_users, a_pos, a_neg):
-        """IGCNTrainer terms on the local batch (users are LOCAL ids)."""
-        rep = self.get_rep()
+        """IGCNTrainer terms on the local batch (users are LOCAL ids); the aux
+        term's gradient joins dE_k inside the propagation backward."""
+        aux_idx = tuple(t.to(torch.int64).contiguous() for t in (a_users, a_pos, a_neg))
+        rep, aux = ShardedPropagate.apply(self.embedding.weight, self.w, self, self.feat_values(), aux_idx)
         bpr, l2 = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_local)
-        aux, _ = ops.bpr_loss(self.embedding.weight, a_users, a_pos, a_neg, 0, self.n_local, w=self.w)
         return bpr, l2, aux
 
     def sync_grads(self):

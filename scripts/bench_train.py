@@ -30,10 +30,19 @@ def main():
     ap.add_argument('--batch', type=int, default=2048)
     ap.add_argument('--batch-rep', default='auto', choices=['auto', 'true', 'false'],
                     help='last layer only at the batch rows (model.batch_rep_pays)')
+    ap.add_argument('--sharded', action='store_true',
+                    help='igr.dist_train.ShardedIGCN (one rank per GPU under torch.distributed.run; '
+                         'per-rank batch --batch)')
     args = ap.parse_args()
     from igr import model as M
     from igr import trainer as T
     from igr.dataset import synthetic_pairs
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    if args.sharded and world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', '0')))
+        dist.init_process_group('nccl')
     dev = torch.device('cuda')
     pairs = synthetic_pairs(args.n_users, args.n_items, args.n_edges, 0)
 
@@ -47,6 +56,8 @@ def main():
             return len(pairs)
     ds = DS()
     t0 = time.time()
+    if args.sharded:
+        return sharded(args, ds, rank, world, dev)
     m = M.IGCN({'name': 'IGCN', 'embedding_size': args.d, 'n_layers': args.layers, 'device': dev, 'dropout': 0.3,
                 'feature_ratio': 1., 'dataset': ds,
                 'batch_rep': {'auto': 'auto', 'true': True, 'false': False}[args.batch_rep]})
@@ -75,6 +86,40 @@ def main():
                       'adj_nnz': m.norm_adj.nnz, 'feat_nnz': m.feat_mat.nnz,
                       'batch_rep': M.batch_rep_pays(m, args.batch),
                       'edges_per_s_fwd_bwd': (m.norm_adj.nnz * args.layers + m.feat_mat.nnz) * 2 * args.steps / el}))
+
+
+def sharded(args, ds, rank, world, dev):
+    import torch.distributed as dist
+    from igr.dist_train import ShardedIGCN, ShardedIGCNTrainer
+    t0 = time.time()
+    m = ShardedIGCN({'embedding_size': args.d, 'n_layers': args.layers, 'device': dev, 'dropout': 0.3,
+                     'feature_ratio': 1., 'dataset': ds}, rank, world)
+    tr = ShardedIGCNTrainer({'batch_size': args.batch, 'l2_reg': 0., 'aux_reg': 0.01, 'lr': 1e-3}, m)
+    print(f'rank {rank}: built in {time.time() - t0:.1f}s: users [{m.u0}, {m.u1})', file=sys.stderr)
+    m.train()
+    for _ in range(args.warmup):
+        tr.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = tr.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    if rank == 0:
+        print(json.dumps({'mode': 'sharded', 'world': world, 'ms_per_step': el / args.steps * 1e3,
+                          'samples_per_s': world * args.batch * args.steps / el, 'loss': float(loss),
+                          'n_users': args.n_users, 'n_items': args.n_items, 'n_edges': args.n_edges, 'd': args.d,
+                          'layers': args.layers}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == '__main__':

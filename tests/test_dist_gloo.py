@@ -16,9 +16,10 @@ from igr.dist import BipartiteShard, balanced_ranges
 from oracle import igr_oracle as O
 
 
-def oracle_spmm(g, x, vals, out, accumulate, add=None, beta=0.0):
-    """The rank-local SpMM restated on the CPU: out = A x (+ out) (+ beta add).
-    vals are by edge id (a reverse graph carries the forward edge ids)."""
+def oracle_spmm(g, x, vals, out, accumulate, add=None, beta=0.0, acc=None, acc_mode=0, acc_div=1.0):
+    """The rank-local SpMM restated on the CPU: out = A x (+ out) (+ beta add),
+    acc = out (mode 1) / (acc + out) / acc_div (mode 2).  vals are by edge id
+    (a reverse graph carries the forward edge ids)."""
     h = g.host()
     v = vals.numpy() if h['edge_id'] is None else vals.numpy()[h['edge_id']]
     A = O.CSR(g.n_rows, g.n_cols, h['row_ptr'], h['col_idx'].astype(np.int64), v)
@@ -29,6 +30,11 @@ def oracle_spmm(g, x, vals, out, accumulate, add=None, beta=0.0):
         out.copy_(y)
     if add is not None:
         out.add_(beta * add)
+    if acc is not None:
+        if acc_mode == 1:
+            acc.copy_(out)
+        else:
+            acc.add_(out).div_(acc_div)
     return out
 
 

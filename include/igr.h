@@ -205,6 +205,20 @@ int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint32_t *bits, 
                              int32_t self_add, float *out, int64_t ldo, void *stream);
 int igr_rowset_clear(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, void *stream);
 
+/* Eval ranking (BasicTrainer.eval, trainer.py:146-182): scores of a user batch
+ * against every item (igr_gemm_f32), the user's train (and for 'test' val)
+ * items set to -inf, then the top k per user.
+ *   igr_mask_scores_f32: scores[r * ld + cols[p]] = -inf, p in [row_ptr[r], row_ptr[r+1])
+ *                        (row_ptr may point into a larger CSR: absolute offsets)
+ *   igr_topk_f32: out_idx[r*k + s] / out_val[r*k + s] (out_val nullable) = the k
+ *                 largest of scores[r, 0:n_cols], ordered by value descending,
+ *                 ties by index ascending (deterministic); 1 <= k <= min(1024, n_cols);
+ *                 one workgroup per row, radix select + LDS bitonic sort. */
+int igr_mask_scores_f32(int64_t n_rows, const int64_t *row_ptr, const int32_t *cols, float *scores, int64_t ld,
+                        void *stream);
+int igr_topk_f32(int64_t n_rows, int64_t n_cols, const float *scores, int64_t ld, int32_t k, float *out_val,
+                 int64_t *out_idx, void *stream);
+
 /* The uniforms igr_spmm_scaled_f32 draws for edge ids 0..n-1 (for tests and
  * for an explicit-values replay of the same mask). */
 int igr_dropout_uniforms(int64_t n, uint64_t seed, uint64_t offset, float *out, void *stream);

@@ -267,6 +267,33 @@ def scatter_add_rows(dst, idx, src, offset=0):
     return dst
 
 
+def mask_scores(scores, row_ptr, cols):
+    """scores[r, cols[row_ptr[r]:row_ptr[r+1]]] = -inf in place (row_ptr: int64
+    [n_rows + 1], absolute offsets into cols, e.g. a slice of a whole CSR)."""
+    _dev(scores, row_ptr, cols)
+    _f32(scores)
+    if scores.stride(1) != 1:
+        raise IgrError('mask_scores: scores need unit inner stride')
+    n = scores.shape[0]
+    if row_ptr.numel() < n + 1:
+        raise IgrError('mask_scores: row_ptr needs n_rows + 1 entries')
+    L.call('igr_mask_scores_f32', n, _p(row_ptr), _p(cols), _p(scores), scores.stride(0), _stream())
+    return scores
+
+
+def topk(scores, k, values=True):
+    """Per-row top k (value descending, ties by index ascending): (values, indices int64)."""
+    _dev(scores)
+    _f32(scores)
+    if scores.dim() != 2 or scores.stride(1) != 1:
+        raise IgrError('topk: 2-D scores with unit inner stride expected')
+    n, m = scores.shape
+    idx = torch.empty(n, k, dtype=torch.int64, device=scores.device)
+    val = torch.empty(n, k, dtype=torch.float32, device=scores.device) if values else None
+    L.call('igr_topk_f32', n, m, _p(scores), scores.stride(0), int(k), _p(val), _p(idx), _stream())
+    return val, idx
+
+
 def gemm(a, b, bias=None, trans_a=False, trans_b=False):
     """C = A(m,k) B(k,n) + bias; b is [n, k] (Linear weight) unless trans_b."""
     _dev(a, b, bias)

@@ -25,6 +25,7 @@ import torch.nn.functional as F
 from torch.optim import SGD  # noqa: F401  (resolved by name, trainer.py:44-46)
 from torch.optim import Adam as TorchAdam  # noqa: F401
 
+from . import ops
 from .dataset import AuxiliaryDataset, BPRBatchSampler
 from .optim import Adam  # noqa: F401  fused HIP Adam, resolved by name 'Adam'
 from .sampler import DeviceBPRSampler
@@ -156,7 +157,10 @@ class BasicTrainer:
     @torch.no_grad()
     def rank(self, val_or_test, banned_items=None):
         """Top-max(topks) items per user, train items (and val items for
-        'test') excluded except for split 'train' (trainer.py:146-170)."""
+        'test') excluded except for split 'train' (trainer.py:146-170).
+        One propagation per eval; per 512-user batch: MFMA score GEMM,
+        igr_mask_scores (the exclusion CSR is uploaded once, each batch passes
+        its slice of row_ptr) and igr_topk (value desc, ties by index asc)."""
         self.model.eval()
         n_users = self.dataset.n_users
         rep = self.model.get_rep()
@@ -165,7 +169,9 @@ class BasicTrainer:
             lists = self.dataset.train_data
             if val_or_test == 'test':
                 lists = [a + b for a, b in zip(self.dataset.train_data, self.dataset.val_data)]
-            excl = _csr(lists, n_users)
+            ptr, flat = _csr(lists, n_users)
+            excl = (torch.from_numpy(ptr.astype(np.int64)).to(self.device),
+                    torch.from_numpy(flat.astype(np.int32)).to(self.device))
         kmax = max(self.topks)
         rec = []
         for s in range(0, n_users, self.test_batch_size):
@@ -173,14 +179,10 @@ class BasicTrainer:
             users = torch.arange(s, e, dtype=torch.int64, device=self.device)
             scores = self.model.predict(users, rep)
             if excl is not None:
-                ptr, flat = excl
-                cnt = np.diff(ptr[s:e + 1])
-                r = torch.from_numpy(np.repeat(np.arange(e - s), cnt)).to(self.device)
-                c = torch.from_numpy(flat[ptr[s]:ptr[e]]).to(self.device)
-                scores[r, c] = -np.inf
+                ops.mask_scores(scores, excl[0][s:e + 1], excl[1])
             if banned_items is not None:
                 scores[:, torch.as_tensor(banned_items, device=self.device)] = -np.inf
-            _, items = torch.topk(scores, k=kmax)
+            _, items = ops.topk(scores, kmax, values=False)
             rec.append(items.cpu().numpy())
         return np.concatenate(rec, axis=0)
 

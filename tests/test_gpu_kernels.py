@@ -432,3 +432,38 @@ def test_spmm_pull_filter_collisions_large_graph():
     close(y, ref, atol_row=2e-6)
     bits, filt, _ = ops._rowset(g)
     assert int(bits.abs().sum()) == 0 and int(filt.abs().sum()) == 0
+
+
+@pytest.mark.parametrize('n,m,k', [(37, 3706, 20), (5, 1_000_003, 100), (64, 130, 128), (8, 1, 1), (9, 1500, 1024)])
+def test_topk_matches_sorted_reference(n, m, k):
+    """igr_topk: the k largest per row, value descending, ties by index ascending
+    (checked against a stable numpy sort), with many exact ties and -inf."""
+    rng = np.random.default_rng(m % 1000 + k)
+    s = rng.standard_normal((n, m)).astype(np.float32)
+    s[:, ::7] = np.round(s[:, ::7], 1)  # exact ties
+    if m > 10:
+        s[0, :] = -np.inf  # a row of only -inf: the k smallest indices
+        s[1, : m // 2] = 0.5  # more ties at the k-th value than needed
+    val, idx = ops.topk(t(s), k)
+    order = np.lexsort((np.broadcast_to(np.arange(m), s.shape), -s.astype(np.float64)), axis=1)[:, :k]
+    np.testing.assert_array_equal(idx.cpu().numpy(), order)
+    np.testing.assert_array_equal(val.cpu().numpy(), np.take_along_axis(s, order, 1))
+
+
+def test_mask_scores_then_topk_matches_torch():
+    """mask (absolute row_ptr slice into a bigger CSR) + topk == torch masking + sort."""
+    rng = np.random.default_rng(2)
+    n_all, m, k = 50, 400, 20
+    lists = [sorted(set(rng.integers(0, m, rng.integers(0, 60)).tolist())) for _ in range(n_all)]
+    ptr = np.concatenate([[0], np.cumsum([len(x) for x in lists])]).astype(np.int64)
+    flat = np.array([i for x in lists for i in x], dtype=np.int32)
+    s0, s1 = 10, 30
+    sc = rng.standard_normal((s1 - s0, m)).astype(np.float32)
+    gs = t(sc)
+    ops.mask_scores(gs, t(ptr)[s0:s1 + 1], t(flat))
+    ref = sc.copy()
+    for r in range(s1 - s0):
+        ref[r, lists[s0 + r]] = -np.inf
+    np.testing.assert_array_equal(gs.cpu().numpy(), ref)
+    _, idx = ops.topk(gs, k)
+    np.testing.assert_array_equal(idx.cpu().numpy(), np.argsort(-ref, axis=1, kind='stable')[:, :k])

@@ -292,10 +292,14 @@ int igr_bpr_fwd_bwd_f32(int64_t batch, int32_t d, const int64_t *users, const in
  * B(k, n) = b[n*ldb + k] (trans_b = 0: nn.Linear weight [N, K]) or
  *           b[k*ldb + n] (trans_b = 1).  bias nullable.
  * The d x d / d x 4d projections of NGCF (model.py:4039) and AttIGCN
- * (model.py:4259, 4264), forward and backward. */
+ * (model.py:4259, 4264), forward and backward.  Outputs with few 64 x 64
+ * tiles and a long K (the weight gradients, K = node count) split K over
+ * workgroups when `workspace` holds igr_gemm_workspace_size(m, n, k) bytes
+ * (NULL / smaller: no split); the splits are summed in order (deterministic). */
+int64_t igr_gemm_workspace_size(int64_t m, int64_t n, int64_t k);
 int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int64_t lda, int32_t trans_a,
                  const float *b, int64_t ldb, int32_t trans_b, const float *bias, float *c,
-                 int64_t ldc, void *stream);
+                 int64_t ldc, void *workspace, int64_t ws_bytes, void *stream);
 
 /* ------------------------------------------------------- training step */
 

@@ -4,7 +4,9 @@
 // (model.py:3998-4004, 4039) and AttIGCN weight_q / weight_k Linear(d, 4d)
 // (model.py:4242-4243, 4259, 4264), forward and backward.  Shapes are tall and
 // skinny (M = node count, N, K = d..4d), so one 64x64 output tile per
-// workgroup, K staged through LDS 16 at a time.  f32-input MFMA is an exact
+// workgroup, K staged through LDS 16 at a time.  The weight gradients
+// (M, N = d..4d, K = node count) have only a few output tiles: there K is
+// split over workgroups (grid.z) into a workspace and summed in split order.  f32-input MFMA is an exact
 // k-ordered fmaf chain (no xf32 on gfx950), i.e. fp32 semantics.
 #include "common.h"
 
@@ -19,7 +21,13 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(int64_t M, int64_t N, int64
                                                      const float *__restrict__ A, int64_t lda,
                                                      const float *__restrict__ B, int64_t ldb,
                                                      const float *__restrict__ bias,
-                                                     float *__restrict__ C, int64_t ldc) {
+                                                     float *__restrict__ C, int64_t ldc, int64_t kc,
+                                                     int64_t zstride) {
+    // split-K: this workgroup takes K range [z kc, min(K, (z+1) kc)) and writes
+    // its partial tile to C + z * zstride (kc = K, zstride = 0 without a split)
+    const int64_t k_lo = (int64_t)blockIdx.z * kc;
+    const int64_t k_hi = k_lo + kc < K ? k_lo + kc : K;
+    C += (int64_t)blockIdx.z * zstride;
     // LDS images [k][m] and [k][n], padded by one float to break bank strides.
     __shared__ float As[BK][BM + 1];
     __shared__ float Bs[BK][BN + 1];
@@ -33,7 +41,7 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(int64_t M, int64_t N, int64
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int64_t k0 = 0; k0 < K; k0 += BK) {
+    for (int64_t k0 = k_lo; k0 < k_hi; k0 += BK) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int idx = t + i * 256;
@@ -42,14 +50,14 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(int64_t M, int64_t N, int64
             else { mm = idx / BK; kk = idx % BK; }      // a[m*lda + k]: k contiguous
             const int64_t gm = m0 + mm, gk = k0 + kk;
             float v = 0.f;
-            if (gm < M && gk < K) v = TA ? A[gk * lda + gm] : A[gm * lda + gk];
+            if (gm < M && gk < k_hi) v = TA ? A[gk * lda + gm] : A[gm * lda + gk];
             As[kk][mm] = v;
             int nn;
             if (TB) { kk = idx / BN; nn = idx % BN; }   // b[k*ldb + n]
             else { nn = idx / BK; kk = idx % BK; }      // b[n*ldb + k] (Linear weight)
             const int64_t gn = n0 + nn, gk2 = k0 + kk;
             float w = 0.f;
-            if (gn < N && gk2 < K) w = TB ? B[gk2 * ldb + gn] : B[gn * ldb + gk2];
+            if (gn < N && gk2 < k_hi) w = TB ? B[gk2 * ldb + gn] : B[gn * ldb + gk2];
             Bs[kk][nn] = w;
         }
         __syncthreads();
@@ -85,13 +93,42 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(int64_t M, int64_t N, int64
         }
 }
 
+// C[m, n] = bias[n] + sum_z W[z, m, n], z in order (deterministic split-K reduce)
+__global__ void splitk_reduce(int64_t M, int64_t N, int S, const float *__restrict__ W,
+                              const float *__restrict__ bias, float *__restrict__ C, int64_t ldc) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= M * N) return;
+    const int64_t m = t / N, n = t - m * N;
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += W[(int64_t)z * M * N + t];
+    C[m * ldc + n] = s + (bias ? bias[n] : 0.f);
+}
+
+// Split count: enough workgroups to fill the chip when the output has few
+// 64x64 tiles and K is long (e.g. a Linear weight gradient, K = node count).
+static int split_count(int64_t m, int64_t n, int64_t k) {
+    const int64_t tiles = ((m + BM - 1) / BM) * ((n + BN - 1) / BN);
+    if (tiles >= 256 || k < 1024) return 1;
+    int64_t s = (512 + tiles - 1) / tiles;
+    const int64_t smax = k / 256;  // at least 256 of K per split
+    if (s > smax) s = smax;
+    if (s > 256) s = 256;
+    return s < 1 ? 1 : (int)s;
+}
+
 }  // namespace igr
 
 using namespace igr;
 
+extern "C" int64_t igr_gemm_workspace_size(int64_t m, int64_t n, int64_t k) {
+    const int s = (m > 0 && n > 0 && k > 0) ? split_count(m, n, k) : 1;
+    return s > 1 ? (int64_t)s * m * n * (int64_t)sizeof(float) : 0;
+}
+
 extern "C" int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int64_t lda,
                             int32_t trans_a, const float *b, int64_t ldb, int32_t trans_b,
-                            const float *bias, float *c, int64_t ldc, void *stream) {
+                            const float *bias, float *c, int64_t ldc, void *workspace, int64_t ws_bytes,
+                            void *stream) {
     return guarded("igr_gemm_f32", [&]() -> int {
         const char *fn = "igr_gemm_f32";
         if (m < 0 || n < 0 || k < 0) return arg_error(fn, "negative size");
@@ -101,15 +138,25 @@ extern "C" int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int
         if (m == 0 || n == 0) return IGR_OK;
         if ((n + BN - 1) / BN > 65535) return arg_error(fn, "n too large");
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-        dim3 grid((unsigned)((m + BM - 1) / BM), (unsigned)((n + BN - 1) / BN));
-        if (trans_a && trans_b)
-            hipLaunchKernelGGL((gemm_f32_mfma<true, true>), grid, dim3(256), 0, st, m, n, k, a, lda, b, ldb, bias, c, ldc);
-        else if (trans_a)
-            hipLaunchKernelGGL((gemm_f32_mfma<true, false>), grid, dim3(256), 0, st, m, n, k, a, lda, b, ldb, bias, c, ldc);
-        else if (trans_b)
-            hipLaunchKernelGGL((gemm_f32_mfma<false, true>), grid, dim3(256), 0, st, m, n, k, a, lda, b, ldb, bias, c, ldc);
-        else
-            hipLaunchKernelGGL((gemm_f32_mfma<false, false>), grid, dim3(256), 0, st, m, n, k, a, lda, b, ldb, bias, c, ldc);
+        int S = split_count(m, n, k);
+        if (S > 1 && (!workspace || ws_bytes < (int64_t)S * m * n * (int64_t)sizeof(float))) S = 1;
+        const int64_t kc = S > 1 ? (((k + S - 1) / S + BK - 1) / BK) * BK : k;
+        if (S > 1) S = (int)((k + kc - 1) / kc);  // BK-rounded slices may need fewer splits
+        float *out = S > 1 ? static_cast<float *>(workspace) : c;
+        const int64_t ldo = S > 1 ? n : ldc, zs = S > 1 ? m * n : 0;
+        const float *bo = S > 1 ? nullptr : bias;
+        dim3 grid((unsigned)((m + BM - 1) / BM), (unsigned)((n + BN - 1) / BN), (unsigned)S);
+#define IGR_GEMM(TA_, TB_)                                                                                   \
+    hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_>), grid, dim3(256), 0, st, m, n, k, a, lda, b, ldb, bo, out, ldo, \
+                       kc, zs)
+        if (trans_a && trans_b) IGR_GEMM(true, true);
+        else if (trans_a) IGR_GEMM(true, false);
+        else if (trans_b) IGR_GEMM(false, true);
+        else IGR_GEMM(false, false);
+#undef IGR_GEMM
+        if (S > 1)
+            hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((m * n + 255) / 256)), dim3(256), 0, st, m, n, S,
+                               static_cast<const float *>(workspace), bias, c, ldc);
         return launch_status(fn);
     });
 }

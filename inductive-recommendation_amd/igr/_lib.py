@@ -77,8 +77,9 @@ SIGNATURES = {
     'igr_scatter_add_rows_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     'igr_bpr_fwd_bwd_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,
                                            c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    'igr_gemm_workspace_size': (c_i64, [c_i64, c_i64, c_i64]),
     'igr_gemm_f32': (ctypes.c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp, c_vp,
-                                    c_i64, c_vp]),
+                                    c_i64, c_vp, c_i64, c_vp]),
     'igr_bpr_sample': (ctypes.c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, ctypes.c_uint64, ctypes.c_uint64,
                                       c_i32, c_vp, c_vp, c_vp, c_vp]),
     'igr_adam_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,

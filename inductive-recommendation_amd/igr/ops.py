@@ -304,8 +304,10 @@ def gemm(a, b, bias=None, trans_a=False, trans_b=False):
     if kb != k:
         raise IgrError(f'gemm inner dims differ: {k} vs {kb}')
     c = torch.empty(m, n, dtype=torch.float32, device=a.device)
+    wsb = int(L.lib().igr_gemm_workspace_size(m, n, k))  # split-K workspace (few output tiles, long K)
+    ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=a.device) if wsb > 0 else None
     L.call('igr_gemm_f32', m, n, k, _p(a), a.stride(0), int(trans_a), _p(b), b.stride(0), int(trans_b),
-           _p(None if bias is None else bias.contiguous()), _p(c), c.stride(0), _stream())
+           _p(None if bias is None else bias.contiguous()), _p(c), c.stride(0), _p(ws), wsb, _stream())
     return c
 
 

@@ -30,6 +30,8 @@ def main():
     ap.add_argument('--batch', type=int, default=2048)
     ap.add_argument('--batch-rep', default='auto', choices=['auto', 'true', 'false'],
                     help='last layer only at the batch rows (model.batch_rep_pays)')
+    ap.add_argument('--model', default='IGCN', choices=['IGCN', 'AttIGCN', 'LightGCN'])
+    ap.add_argument('--eval', action='store_true', help='also time one full eval ranking (Recall@20 path)')
     ap.add_argument('--sharded', action='store_true',
                     help='igr.dist_train.ShardedIGCN (one rank per GPU under torch.distributed.run; '
                          'per-rank batch --batch)')
@@ -58,19 +60,23 @@ def main():
     t0 = time.time()
     if args.sharded:
         return sharded(args, ds, rank, world, dev)
-    m = M.IGCN({'name': 'IGCN', 'embedding_size': args.d, 'n_layers': args.layers, 'device': dev, 'dropout': 0.3,
-                'feature_ratio': 1., 'dataset': ds,
-                'batch_rep': {'auto': 'auto', 'true': True, 'false': False}[args.batch_rep]})
+    m = getattr(M, args.model)({'name': args.model, 'embedding_size': args.d, 'n_layers': args.layers,
+                                'device': dev, 'dropout': 0.3, 'feature_ratio': 1., 'dataset': ds,
+                                'batch_rep': {'auto': 'auto', 'true': True, 'false': False}[args.batch_rep]})
     # AuxiliaryDataset needs per-user lists; with feature_ratio = 1 it is the dataset itself
     T.AuxiliaryDataset = lambda dataset, um, im: dataset
-    tr = T.get_trainer({'name': 'IGCNTrainer', 'optimizer': 'Adam', 'lr': 1e-3, 'l2_reg': 0., 'aux_reg': 0.01,
-                        'device': dev, 'n_epochs': 1, 'batch_size': args.batch, 'test_batch_size': 512,
-                        'topks': [20]}, ds, m)
-    print(f'built in {time.time() - t0:.1f}s: adj nnz {m.norm_adj.nnz}, feat nnz {m.feat_mat.nnz}', file=sys.stderr)
+    igcn = args.model != 'LightGCN'
+    tr = T.get_trainer({'name': 'IGCNTrainer' if igcn else 'BPRTrainer', 'optimizer': 'Adam', 'lr': 1e-3,
+                        'l2_reg': 0., 'aux_reg': 0.01, 'device': dev, 'n_epochs': 1, 'batch_size': args.batch,
+                        'test_batch_size': 512, 'topks': [20]}, ds, m)
+    print(f'built in {time.time() - t0:.1f}s: adj nnz {m.norm_adj.nnz}' +
+          (f', feat nnz {m.feat_mat.nnz}' if igcn else ''), file=sys.stderr)
     m.train()
 
     def step():
         u, p, n = tr.sampler.sample(args.batch)
+        if not igcn:
+            return tr.step(u, p, n)
         au, ap_, an = tr.aux_sampler.sample(args.batch)
         return tr.step(u, p, n, au, ap_, an)
     for _ in range(args.warmup):
@@ -81,11 +87,23 @@ def main():
         loss = step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    print(json.dumps({'ms_per_step': el / args.steps * 1e3, 'loss': float(loss), 'n_users': args.n_users,
-                      'n_items': args.n_items, 'n_edges': args.n_edges, 'd': args.d, 'layers': args.layers,
-                      'adj_nnz': m.norm_adj.nnz, 'feat_nnz': m.feat_mat.nnz,
-                      'batch_rep': M.batch_rep_pays(m, args.batch),
-                      'edges_per_s_fwd_bwd': (m.norm_adj.nnz * args.layers + m.feat_mat.nnz) * 2 * args.steps / el}))
+    feat_nnz = m.feat_mat.nnz if igcn else 0
+    out = {'model': args.model, 'ms_per_step': el / args.steps * 1e3, 'loss': float(loss), 'n_users': args.n_users,
+           'n_items': args.n_items, 'n_edges': args.n_edges, 'd': args.d, 'layers': args.layers,
+           'adj_nnz': m.norm_adj.nnz, 'feat_nnz': feat_nnz,
+           'batch_rep': M.batch_rep_pays(m, args.batch) if args.model == 'IGCN' or not igcn else False,
+           'edges_per_s_fwd_bwd': (m.norm_adj.nnz * args.layers + feat_nnz) * 2 * args.steps / el}
+    if args.eval:
+        # one eval ranking over every user (rep once, MFMA scores, mask, top-k); no held-out lists in
+        # the synthetic data, so the 'train' split (no exclusion) is timed
+        tr.dataset.val_data = tr.dataset.test_data = None
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rec = tr.rank('train')
+        torch.cuda.synchronize()
+        out['eval_rank_s'] = time.perf_counter() - t0
+        out['eval_users'] = int(rec.shape[0])
+    print(json.dumps(out))
 
 
 def sharded(args, ds, rank, world, dev):

@@ -467,3 +467,22 @@ def test_mask_scores_then_topk_matches_torch():
     np.testing.assert_array_equal(gs.cpu().numpy(), ref)
     _, idx = ops.topk(gs, k)
     np.testing.assert_array_equal(idx.cpu().numpy(), np.argsort(-ref, axis=1, kind='stable')[:, :k])
+
+
+@pytest.mark.parametrize('m,n,k', [(256, 64, 9750), (64, 64, 20000), (130, 33, 5000), (300, 200, 1100)])
+def test_gemm_split_k_matches_float64(m, n, k):
+    """Few output tiles x long K (a Linear weight gradient, K = node count): K split
+    over workgroups into a workspace, summed in order; every transposition and bias."""
+    from igr import _lib
+    assert _lib.lib().igr_gemm_workspace_size(m, n, k) > 0  # the split path is taken
+    rng = np.random.default_rng(m + k)
+    A = rng.standard_normal((m, k)).astype(np.float32)
+    B = rng.standard_normal((k, n)).astype(np.float32)
+    bias = rng.standard_normal(n).astype(np.float32)
+    ref = A.astype(np.float64) @ B.astype(np.float64) + bias
+    for ta in (False, True):
+        for tb in (False, True):
+            a = A.T.copy() if ta else A
+            b = B if tb else B.T.copy()
+            c = ops.gemm(t(a), t(b), t(bias), trans_a=ta, trans_b=tb).cpu().numpy()
+            close(c, ref, rtol=1e-5, atol_row=1e-5)

@@ -133,12 +133,7 @@ class ShardedPropagate(torch.autograd.Function):
             acc[nk:].div_(L1)
         aux_loss = None
         if aux is not None:
-            au, ap, an = aux
-            loss = torch.empty(au.numel(), dtype=torch.float32, device=emb.device)
-            ops.L.call('igr_bpr_fwd_bwd_f32', au.numel(), d, ops._p(au), ops._p(ap), ops._p(an), 0, nk,
-                       ops._p(emb), emb.stride(0), ops._p(w), ops._p(loss), None, 0.0, 0.0, None, None, None, 0,
-                       None, ops._stream())
-            aux_loss = loss.mean()
+            aux_loss = model.aux_forward(emb, w, aux)
         return (acc, aux_loss) if aux is not None else acc
 
     @staticmethod
@@ -166,19 +161,135 @@ class ShardedPropagate(torch.autograd.Function):
         model.feat_spmm(fs.graph.reverse(), x, fvals, demb, reverse=True)
         dw = None
         if ctx.aux is not None and g_aux is not None:
-            au, ap, an = ctx.aux
-            dw = torch.zeros_like(w)
-            g_aux = g_aux.float().contiguous()
-            ops.L.call('igr_bpr_fwd_bwd_f32', au.numel(), emb.shape[1], ops._p(au), ops._p(ap), ops._p(an), 0, nk,
-                       ops._p(emb), emb.stride(0), ops._p(w), None, None, 1.0 / au.numel(), 0.0, ops._p(g_aux),
-                       None, ops._p(demb), demb.stride(0), ops._p(dw), ops._stream())
+            dw = model.aux_backward(emb, w, ctx.aux, g_aux, demb)
         return demb, dw, None, None, None
+
+
+class ShardedPropagateRows(torch.autograd.Function):
+    """rep at the local batch rows [users (local ids); items_b] with the LAST
+    layer computed only there (the single-GPU ops.PropagateRows on the shard).
+
+    Forward: x_0 .. x_{L-1} in full (one item all-reduce per layer), then
+      users  rep[u] = ((A x)[u] + x[u] + sum_{l<L-1} x_l[u]) / (L+1)   spmm_rows, local
+      items  every rank's batch items are all-gathered; each rank computes its
+             partial (A x)[i] at all of them on its item block (spmm_rows) and
+             ONE small all-reduce (world x 2B x d) completes them.
+    Backward, first layer as masked pulls (no full SpMM):
+      users  dX[U_k] = A[U_k, I] G_I (every rank's item gradients, all-gathered)
+             + G at the local batch users
+      items  dX[I]   = sum_k (A[I, U_k] G_{U_k} + own item terms)  (one I x d reduce)
+    then L-1 full layers with the batch terms scattered back in, and F^T."""
+
+    @staticmethod
+    def forward(ctx, emb, w, model, fvals, aux, rows_u, items_b):
+        sh, fs, L, spmm, group = model.shard, model.feat, model.n_layers, model.spmm, model.group
+        R = model.rowops
+        ctx.model, ctx.fvals, ctx.aux = model, fvals, aux
+        nk, I = fs.n_local, fs.n_items
+        d = emb.shape[1]
+        L1 = float(L + 1)
+        world = model.world
+        if world > 1:
+            items_all = torch.empty(world * items_b.numel(), dtype=torch.int64, device=emb.device)
+            dist.all_gather_into_tensor(items_all, items_b, group=group)
+        else:
+            items_all = items_b
+        ctx.save_for_backward(emb if aux is not None else None, w, rows_u, items_b, items_all)
+        x = torch.empty(nk + I, d, dtype=torch.float32, device=emb.device)
+        model.feat_spmm(fs.graph, emb, fvals, x)
+        pend = [_allreduce(x[nk:], group, async_op=True)] if world > 1 else []
+        su = si = None
+        bufs = [torch.empty_like(x), torch.empty_like(x)]
+        for layer in range(L - 1):
+            y = bufs[layer % 2]
+            sh.layer(x[:nk], x[nk:], y_users=y[:nk], y_items=y[nk:], group=group, spmm=spmm, pending=pend)
+            pend = []
+            gu, gi = R.gather(x[:nk], rows_u), R.gather(x[nk:], items_b)
+            su = gu if su is None else su.add_(gu)
+            si = gi if si is None else si.add_(gi)
+            x = y
+        for wk in pend:
+            wk.wait()
+        rep_u = R.rows(sh.user_block, x[nk:], rows_u, sh.user_vals, add_g=x[:nk], add_i=su, scale=1.0 / L1)
+        part = R.rows(sh.item_block, x[:nk], items_all, sh.item_vals)
+        if world > 1:
+            _allreduce(part, group)
+        own = part[model.rank * items_b.numel():(model.rank + 1) * items_b.numel()]
+        rep_i = own.add_(R.gather(x[nk:], items_b))
+        if si is not None:
+            rep_i.add_(si)
+        rep_i.div_(L1)
+        rep = torch.cat([rep_u, rep_i])
+        aux_loss = None
+        if aux is not None:
+            aux_loss = model.aux_forward(emb, w, aux)
+        return (rep, aux_loss) if aux is not None else rep
+
+    @staticmethod
+    def backward(ctx, g, g_aux=None):
+        model, fvals = ctx.model, ctx.fvals
+        emb, w, rows_u, items_b, items_all = ctx.saved_tensors
+        sh, fs, L, spmm, group = model.shard, model.feat, model.n_layers, model.spmm, model.group
+        R = model.rowops
+        nk, I = fs.n_local, fs.n_items
+        B = rows_u.numel()
+        L1 = float(L + 1)
+        gs = g.contiguous() / L1
+        gu, gi = gs[:B], gs[B:]
+        if model.world > 1:
+            gi_all = torch.empty(model.world * gi.shape[0], gi.shape[1], dtype=gi.dtype, device=gi.device)
+            dist.all_gather_into_tensor(gi_all, gi.contiguous(), group=group)
+        else:
+            gi_all = gi
+        x = torch.empty(nk + I, gs.shape[1], dtype=torch.float32, device=gs.device)
+        R.pull(sh.user_block, items_all, gi_all, sh.user_vals, out=x[:nk])
+        R.scatter(x[:nk], rows_u, gu)
+        R.pull(sh.item_block, rows_u, gu, sh.item_vals, out=x[nk:])
+        R.scatter(x[nk:], items_b, gi)
+        if model.world > 1:
+            _allreduce(x[nk:], group)
+        if L > 1:
+            gi_dense = torch.zeros(I, gs.shape[1], dtype=torch.float32, device=gs.device)
+            R.scatter(gi_dense, items_b, gi)  # own item terms, added to each partial before its reduce
+            bufs = [torch.empty_like(x), x]
+            for layer in range(L - 1):
+                y = bufs[layer % 2]
+                sh.layer(x[:nk], x[nk:], y_users=y[:nk], y_items=y[nk:], group=group, spmm=spmm,
+                         add_items=gi_dense, beta=1.0)
+                R.scatter(y[:nk], rows_u, gu)
+                x = y
+        demb = torch.empty(fs.graph.n_cols, gs.shape[1], dtype=torch.float32, device=gs.device)
+        model.feat_spmm(fs.graph.reverse(), x, fvals, demb, reverse=True)
+        dw = None
+        if ctx.aux is not None and g_aux is not None:
+            dw = model.aux_backward(emb, w, ctx.aux, g_aux, demb)
+        return demb, dw, None, None, None, None, None
+
+
+class _HipRowOps:
+    """The row kernels of the batch-row path (the CPU gloo tests pass a numpy restatement)."""
+
+    @staticmethod
+    def rows(g, x, rows, vals, add_g=None, add_i=None, scale=1.0):
+        return ops.spmm_rows(g, x, rows, vals, add_g=add_g, add_i=add_i, scale=scale)
+
+    @staticmethod
+    def pull(g, rows, src, vals, out):
+        return ops.spmm_pull(g, rows, src, vals, out=out)
+
+    @staticmethod
+    def gather(x, idx):
+        return ops.gather_rows(x, idx)
+
+    @staticmethod
+    def scatter(dst, idx, src):
+        return ops.scatter_add_rows(dst, idx, src)
 
 
 class ShardedIGCN(nn.Module):
     """IGCN (model.py:4107-4220) on one rank's shard; feature_ratio = 1."""
 
-    def __init__(self, model_config, rank, world, group=None, spmm=None):
+    def __init__(self, model_config, rank, world, group=None, spmm=None, rowops=None):
         super().__init__()
         ds = model_config['dataset']
         if model_config.get('feature_ratio', 1.) != 1.:
@@ -193,7 +304,10 @@ class ShardedIGCN(nn.Module):
         self.alpha, self.delta = 1., model_config.get('delta', 0.99)
         self.rank, self.world, self.group = rank, world, group
         self.spmm = spmm or _hip_spmm
+        self.rowops = rowops or _HipRowOps
         self.hip = spmm is None
+        # last layer only at the batch rows (ShardedPropagateRows); 'batch_rep' False = full layers
+        self.batch_rows = bool(model_config.get('batch_rep', True)) and self.n_layers > 0
         pairs = train_pairs(ds)
         self.shard = BipartiteShard(pairs, self.n_users, self.n_items, rank, world, self.device, d=d)
         self.u0, self.u1 = self.shard.u0, self.shard.u1
@@ -258,9 +372,41 @@ class ShardedIGCN(nn.Module):
         """IGCNTrainer terms on the local batch (users are LOCAL ids); the aux
         term's gradient joins dE_k inside the propagation backward."""
         aux_idx = tuple(t.to(torch.int64).contiguous() for t in (a_users, a_pos, a_neg))
+        if self.batch_rows:
+            users, pos_items, neg_items = (t.to(torch.int64).contiguous() for t in (users, pos_items, neg_items))
+            items_b = torch.cat([pos_items, neg_items])
+            rep, aux = ShardedPropagateRows.apply(self.embedding.weight, self.w, self, self.feat_values(), aux_idx,
+                                                  users, items_b)
+            iu, ip, ineg = ops.batch_positions(users.numel(), users.device)
+            bpr, l2 = ops.bpr_loss(rep, iu, ip, ineg, 0, 0)
+            return bpr, l2, aux
         rep, aux = ShardedPropagate.apply(self.embedding.weight, self.w, self, self.feat_values(), aux_idx)
         bpr, l2 = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_local)
         return bpr, l2, aux
+
+    def aux_forward(self, emb, w, aux):
+        """Mean aux BPR loss on E_k with w (trainer.py:542-549); item features at n_local."""
+        au, ap, an = aux
+        loss = torch.empty(au.numel(), dtype=torch.float32, device=emb.device)
+        ops.L.call('igr_bpr_fwd_bwd_f32', au.numel(), emb.shape[1], ops._p(au), ops._p(ap), ops._p(an), 0,
+                   self.n_local, ops._p(emb), emb.stride(0), ops._p(w), ops._p(loss), None, 0.0, 0.0, None, None,
+                   None, 0, None, ops._stream())
+        return loss.mean()
+
+    def aux_backward(self, emb, w, aux, g_aux, demb):
+        """Adds the aux term's gradient into demb in place; returns d w."""
+        au, ap, an = aux
+        dw = torch.zeros_like(w)
+        g_aux = g_aux.float().contiguous()
+        ops.L.call('igr_bpr_fwd_bwd_f32', au.numel(), emb.shape[1], ops._p(au), ops._p(ap), ops._p(an), 0,
+                   self.n_local, ops._p(emb), emb.stride(0), ops._p(w), None, None, 1.0 / au.numel(), 0.0,
+                   ops._p(g_aux), None, ops._p(demb), demb.stride(0), ops._p(dw), ops._stream())
+        return dw
+
+    def batch_rep(self, users, items_b):
+        """[rep[users]; rep[items_b]] through the batch-row path (no aux term)."""
+        return ShardedPropagateRows.apply(self.embedding.weight, self.w, self, self.feat_values(), None,
+                                          users.to(torch.int64).contiguous(), items_b.to(torch.int64).contiguous())
 
     def sync_grads(self):
         """One all-reduce of the replicated parameters' gradients (item / general rows and w)."""

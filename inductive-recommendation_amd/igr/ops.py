@@ -679,17 +679,21 @@ def propagate_rows(adj, emb, n_layers, rows, feat=None, fvals=None, adj_vals=Non
 _ARANGE = {}
 
 
+def batch_positions(B, device):
+    """(arange(B), B + arange(B), 2B + arange(B)) on `device`, cached."""
+    key = (B, torch.device(device))
+    if key not in _ARANGE:
+        a = torch.arange(3 * B, dtype=torch.int64, device=device)
+        _ARANGE[key] = (a[:B], a[B:2 * B], a[2 * B:])
+    return _ARANGE[key]
+
+
 def batch_rows(users, pos, neg, n_users):
     """Rows of rep a BPR batch reads, and the positions of (users, pos, neg) in
     them: rows = [users, n_users + pos, n_users + neg] (repeats kept - no
     host sync for a unique())."""
-    B = users.numel()
     rows = torch.cat([users.to(torch.int64), pos.to(torch.int64) + n_users, neg.to(torch.int64) + n_users])
-    key = (B, users.device)
-    if key not in _ARANGE:
-        a = torch.arange(3 * B, dtype=torch.int64, device=users.device)
-        _ARANGE[key] = (a[:B], a[B:2 * B], a[2 * B:])
-    return rows, _ARANGE[key]
+    return rows, batch_positions(users.numel(), users.device)
 
 
 def propagate(adj, emb, n_layers, feat=None, fvals=None, adj_vals=None):

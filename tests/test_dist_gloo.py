@@ -190,3 +190,96 @@ def test_sharded_igcn_rep_and_grad_match_unsharded(L):
         np.testing.assert_allclose(rep_k[nk:], rep[U:], **tol)
         np.testing.assert_allclose(grad_k[:nk], grad[u0:u1], **tol)
         np.testing.assert_allclose(grad_k[nk:], grad[U:], **tol)
+
+
+class NumpyRowOps:
+    """The batch-row kernels restated with the oracle SpMM (rows / pull) and torch indexing."""
+
+    @staticmethod
+    def rows(g, x, rows, vals, add_g=None, add_i=None, scale=1.0):
+        y = oracle_spmm(g, x, vals, torch.empty(g.n_rows, x.shape[1]), False)[rows]
+        if add_g is not None:
+            y = y + add_g[rows]
+        if add_i is not None:
+            y = y + add_i
+        return (y * scale).contiguous()
+
+    @staticmethod
+    def pull(g, rows, src, vals, out):
+        S = torch.zeros(g.n_cols, src.shape[1]).index_add_(0, rows, src)
+        return oracle_spmm(g, S, vals, out, False)
+
+    @staticmethod
+    def gather(x, idx):
+        return x[idx].contiguous()
+
+    @staticmethod
+    def scatter(dst, idx, src):
+        return dst.index_add_(0, idx, src)
+
+
+def _rows_worker(rank, world, port, pairs, U, I, d, L, B, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from igr.dist_train import ShardedIGCN
+        m = ShardedIGCN({'dataset': _DS(pairs, U, I), 'embedding_size': d, 'n_layers': L, 'dropout': 0.3,
+                         'device': 'cpu', 'feature_ratio': 1.}, rank, world, spmm=oracle_spmm, rowops=NumpyRowOps)
+        m.eval()
+        g = torch.Generator().manual_seed(0)
+        m.load_full_embedding(torch.randn(U + I + 2, d, generator=g) * 0.1)
+        gr = torch.Generator().manual_seed(10 + rank)
+        users = torch.randint(0, m.n_local, (B,), generator=gr)
+        users[:3] = users[0]  # repeats
+        items = torch.randint(0, I, (2 * B,), generator=gr)
+        items[:4] = 7  # the same item on every rank
+        G = torch.randn(3 * B, d, generator=gr)
+        rep = m.batch_rep(users, items)
+        (rep * G).sum().backward()
+        m.sync_grads()
+        q.put((rank, m.u0, m.u1, users.numpy(), items.numpy(), G.numpy(), rep.detach().numpy(),
+               m.embedding.weight.grad.numpy()))
+    except Exception:
+        import traceback
+        q.put((rank, 'error', traceback.format_exc()))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('L', [1, 3])
+def test_sharded_batch_rows_match_unsharded(L):
+    """World 2, last layer only at the batch rows: users local, items through the
+    all-gathered item list and one small reduce; backward pulls + scattered terms."""
+    rng = np.random.default_rng(5)
+    U, I, d, B = 80, 60, 8, 12
+    pairs = np.stack([rng.integers(0, U, 800), rng.integers(0, I, 800)], 1)
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rows_worker, args=(r, world, port, pairs, U, I, d, L, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != 'error', r[2]
+    A = O.norm_adj(U, I, pairs)
+    F = O.generate_feat(U, I, pairs)
+    fv = O.feat_values(F, 1.0)
+    emb = (torch.randn(U + I + 2, d, generator=torch.Generator().manual_seed(0)) * 0.1).numpy()
+    rep = O.igcn_rep(A, F, fv, emb, L)
+    Gt = np.zeros((U + I, d), np.float32)
+    for rank, u0, u1, users, items, G, _, _ in res:
+        np.add.at(Gt, u0 + users, G[:B])
+        np.add.at(Gt, U + items, G[B:])
+    grad = O.igcn_grad(A, F, fv, L, Gt)
+    tol = dict(rtol=1e-5, atol=1e-6)
+    for rank, u0, u1, users, items, G, rep_b, grad_k in res:
+        nk = u1 - u0
+        np.testing.assert_allclose(rep_b, np.concatenate([rep[u0 + users], rep[U + items]]), **tol)
+        np.testing.assert_allclose(grad_k[:nk], grad[u0:u1], **tol)
+        np.testing.assert_allclose(grad_k[nk:], grad[U:], **tol)

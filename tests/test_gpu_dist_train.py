@@ -75,14 +75,16 @@ def _single(pairs, emb0, batch_lists):
     return losses, m.embedding.weight.detach().cpu().numpy(), m.w.detach().cpu().numpy()
 
 
-def test_sharded_world1_equals_igcn_trainer():
+@pytest.mark.parametrize('batch_rep', [False, True])
+def test_sharded_world1_equals_igcn_trainer(batch_rep):
     from igr.dist_train import ShardedIGCN, ShardedIGCNTrainer
     pairs = _pairs()
     torch.manual_seed(0)
     emb0 = torch.randn(U + I + 2, D) * 0.1
     bl = _batches(1, 0, U)
     ref_losses, ref_emb, ref_w = _single(pairs, emb0.to(DEV), [bl])
-    m = ShardedIGCN(_cfg(DS(pairs)), 0, 1)
+    m = ShardedIGCN(dict(_cfg(DS(pairs)), batch_rep=batch_rep), 0, 1)
+    assert m.batch_rows is batch_rep
     m.load_full_embedding(emb0)
     tr = ShardedIGCNTrainer({'batch_size': B, 'l2_reg': 1e-4, 'aux_reg': 0.01, 'lr': 1e-3}, m)
     m.train()
@@ -101,7 +103,7 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, pairs, emb0, q):
+def _rank(rank, world, port, pairs, emb0, q, batch_rep):
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
@@ -109,7 +111,7 @@ def _rank(rank, world, port, pairs, emb0, q):
     try:
         from igr.dist_train import ShardedIGCN, ShardedIGCNTrainer
         dev = torch.device('cuda')
-        cfg = _cfg(DS(pairs))
+        cfg = dict(_cfg(DS(pairs)), batch_rep=batch_rep)
         m = ShardedIGCN(cfg, rank, world)
         m.load_full_embedding(emb0)
         tr = ShardedIGCNTrainer({'batch_size': B, 'l2_reg': 1e-4, 'aux_reg': 0.01, 'lr': 1e-3}, m)
@@ -128,7 +130,8 @@ def _rank(rank, world, port, pairs, emb0, q):
         dist.destroy_process_group()
 
 
-def test_sharded_world2_one_gpu_equals_single_gpu():
+@pytest.mark.parametrize('batch_rep', [False, True])
+def test_sharded_world2_one_gpu_equals_single_gpu(batch_rep):
     pairs = _pairs()
     torch.manual_seed(0)
     emb0 = torch.randn(U + I + 2, D) * 0.1
@@ -136,7 +139,7 @@ def test_sharded_world2_one_gpu_equals_single_gpu():
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, pairs, emb0, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, pairs, emb0, q, batch_rep)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda r: r[0])

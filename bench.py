@@ -117,7 +117,8 @@ def main():
     del pairs
     nu = shard.u1 - shard.u0
     log(f'shard users [{shard.u0}, {shard.u1}) local nnz {shard.local_nnz} '
-        f'(user block {shard.user_block}, item block {shard.item_block}) ... {time.time() - t0:.1f}s')
+        f'(user block {shard.user_block}, item block nnz {shard.item_nnz} in {len(shard.chunks)} row chunks) '
+        f'... {time.time() - t0:.1f}s')
 
     g = torch.Generator(device=dev).manual_seed(2 + args.seed)
     x_items = torch.randn(I, d, generator=g, device=dev) * 0.1
@@ -195,8 +196,11 @@ def main():
                        'item_source_tiles': shard.item_tiles, 'launches_per_step': nl},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic,
-                         'kernel': f'igr::spmm_main<{d},true,false>',
-                         'avg_launch_ms': avg_kernel_s * 1e3, 'algorithmic_bytes_per_launch': avg_bytes},
+                         'kernel': f'igr::spmm_main<{d}, igr::W_Val>',
+                         'avg_launch_ms': avg_kernel_s * 1e3, 'algorithmic_bytes_per_launch': avg_bytes,
+                         'launches': {n: {'ms': float(kern_ms[:, k].mean()), 'rows': int(r), 'nnz': int(z),
+                                          'algorithmic_GBps': launch_bytes[k] / float(kern_ms[:, k].mean()) / 1e6}
+                                      for k, (n, _g, _s, r, z) in enumerate(launches)}},
             'cpu_baseline': cpu,
         }
         print(json.dumps(out), flush=True)

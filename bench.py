@@ -42,33 +42,64 @@ def spmm_bytes(nnz, n_rows, d):
     return nnz * (4 + 4 + 4 * d) + n_rows * (8 + 4 * d)
 
 
+def _cpu_model():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
 def cpu_baseline(shard, x_users, x_items, d, seconds, sample_edges):
-    """Oracle C SpMM (OpenMP) on the first rows of both blocks, ~sample_edges edges."""
+    """CPU SpMM on the first rows of both blocks (~sample_edges edges of the same graph), as
+    SURVEY §8d asks: (ii) the oracle C SpMM (OpenMP; the primary, kind 'port') for ~2/3 of
+    the budget and (i) torch.sparse.mm with a CSR tensor (the restated gspmm) for the rest."""
     from oracle import igr_oracle as O
     threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
     lib = O.lib()
     parts = []
-    for blk, vals, lhs in [(shard.user_block, shard.user_vals, x_items), (shard.item_block, shard.item_vals, x_users)]:
-        h = blk.host()
-        rp = h['row_ptr']
-        R = int(min(np.searchsorted(rp, sample_edges // 2), blk.n_rows))
+    ih = shard.item_host
+    blocks = [(shard.user_block.host()['row_ptr'], shard.user_block.host()['col_idx'], shard.user_vals, x_items,
+               shard.user_block.n_cols),
+              (ih['row_ptr'], ih['col_idx'], torch.from_numpy(ih['vals']), x_users, shard.u1 - shard.u0)]
+    for rp, ci, vals, lhs, n_cols in blocks:
+        R = int(min(np.searchsorted(rp, sample_edges // 2), len(rp) - 1))
         e = int(rp[R])
-        parts.append((R, np.ascontiguousarray(rp[:R + 1]), h['col_idx'][:e].astype(np.int64),
-                      vals[:e].cpu().numpy(), lhs.cpu().numpy()))
+        parts.append((R, np.ascontiguousarray(rp[:R + 1]), ci[:e].astype(np.int64),
+                      vals[:e].cpu().numpy(), lhs.cpu().numpy(), n_cols))
     edges = sum(int(p[1][-1]) for p in parts)
     outs = [np.empty((p[0], d), np.float32) for p in parts]
     iters, t0 = 0, time.perf_counter()
     while True:
-        for (R, rp, ci, v, x), out in zip(parts, outs):
+        for (R, rp, ci, v, x, _), out in zip(parts, outs):
             lib.orc_spmm_sum_f32(R, d, rp, ci, v, None, x, d, out, d, threads)
         iters += 1
         el = time.perf_counter() - t0
-        if el >= seconds:
+        if el >= seconds * 2 / 3:
+            break
+    # (i) torch.sparse.mm over CSR tensors of the same rows
+    torch.set_num_threads(threads)
+    mats = [(torch.sparse_csr_tensor(torch.from_numpy(rp), torch.from_numpy(ci), torch.from_numpy(v),
+                                     size=(R, n_cols)), torch.from_numpy(x)) for R, rp, ci, v, x, n_cols in parts]
+    t_iters, t1 = 0, time.perf_counter()
+    while True:
+        for A, x in mats:
+            torch.sparse.mm(A, x)
+        t_iters += 1
+        t_el = time.perf_counter() - t1
+        if t_el >= seconds / 3:
             break
     return {'value': edges * iters / el, 'unit': 'edges/s', 'cores': threads, 'kind': 'port',
             'sample': f'{edges} edges (first {parts[0][0]} user rows + first {parts[1][0]} item rows of the same '
                       f'graph), d={d}, {iters} passes in {el:.1f}s, oracle/oracle.c orc_spmm_sum_f32 '
-                      f'(restated DGL CPU SpMMSumCsr, gcc -O2 -fopenmp)'}
+                      f'(restated DGL CPU SpMMSumCsr, gcc -O2 -fopenmp)',
+            'cpu_model': _cpu_model(),
+            'torch_sparse_mm': {'value': edges * t_iters / t_el, 'unit': 'edges/s', 'cores': threads,
+                                'sample': f'same rows, torch.sparse.mm(CSR, dense) on CPU, {t_iters} passes in '
+                                          f'{t_el:.1f}s (the restated gspmm, SURVEY §8d (i))'}}
 
 
 def main():

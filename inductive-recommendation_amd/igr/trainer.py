@@ -187,7 +187,14 @@ class BasicTrainer:
         return np.concatenate(rec, axis=0)
 
     def eval(self, val_or_test, banned_items=None):
-        """trainer.py:146-210; returns (result string, metrics)."""
+        """trainer.py:146-210; returns (result string, metrics).
+
+        The reference iterates its test_user_loader (a torch DataLoader,
+        trainer.py:41-42, 151), and creating a DataLoader iterator draws one
+        int64 base seed from the global CPU generator.  The same draw is made
+        here, so a seeded run stays on the reference's CPU random stream (the
+        dropout masks of dropout_rng='cpu' and anything seeded after an eval)."""
+        torch.empty((), dtype=torch.int64).random_()
         eval_data = getattr(self.dataset, val_or_test + '_data')
         rec_items = self.rank(val_or_test, banned_items)
         metrics = self.calculate_metrics(eval_data, rec_items)

@@ -150,15 +150,19 @@ int igr_spmm_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx, const
 
 /* SpMM with row / column scaled weights and fused dropout:
  *   w(p) = (row_scale ? row_scale[r] : 1) * (col_scale ? col_scale[c] : 1)
- *   if keep < 1: w = floor(keep + U) ? w / keep : 0,  U = uniform(seed, offset, edge id)
+ *   if keep < 1: w = floor(keep + U) ? w / keep : 0,
+ *                U = uniform(seed, offset, key(forward row, forward column))
  * The IGCN feature graph's values are row-constant (row_sum[r]^e,
  * model.py:4127-4130), so its dropout SpMM (model.py:4016-4028, 4184) needs
- * no per-edge array: forward uses row_scale, the reverse graph col_scale, and
- * both draw the same mask from the forward edge id (the reverse graph's
- * edge_id).  Same epilogue / workspace contract as igr_spmm_f32. */
+ * no per-edge array. The mask is keyed by the edge's (row, column) in the
+ * frame it was drawn for (the coalesced feature graph has one edge per
+ * pair); transposed = 1 runs g as the reverse of that frame, so the backward
+ * regenerates the forward's mask without an edge-id permutation.  Rows and
+ * columns < 2^32 when keep < 1.  Same epilogue / workspace contract as
+ * igr_spmm_f32. */
 int igr_spmm_scaled_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx, const float *row_scale,
-                        const float *col_scale, float keep, uint64_t seed, uint64_t offset, float *y,
-                        int64_t ldy, const igr_epilogue *epi, float *workspace, void *stream);
+                        const float *col_scale, float keep, uint64_t seed, uint64_t offset, int32_t transposed,
+                        float *y, int64_t ldy, const igr_epilogue *epi, float *workspace, void *stream);
 
 /* Row-restricted SpMM and its transpose (training step: the loss reads the
  * representation only at the batch rows, model.py:4048-4049 / 4049-4051, so
@@ -219,9 +223,10 @@ int igr_mask_scores_f32(int64_t n_rows, const int64_t *row_ptr, const int32_t *c
 int igr_topk_f32(int64_t n_rows, int64_t n_cols, const float *scores, int64_t ld, int32_t k, float *out_val,
                  int64_t *out_idx, void *stream);
 
-/* The uniforms igr_spmm_scaled_f32 draws for edge ids 0..n-1 (for tests and
- * for an explicit-values replay of the same mask). */
-int igr_dropout_uniforms(int64_t n, uint64_t seed, uint64_t offset, float *out, void *stream);
+/* The uniforms igr_spmm_scaled_f32 draws, per CSR position of g (out[nnz];
+ * for tests and for an explicit-values replay of the same mask). */
+int igr_dropout_uniforms(const igr_csr *g, uint64_t seed, uint64_t offset, int32_t transposed, float *out,
+                         void *stream);
 
 /* u_dot_v SDDMM: out[eid(p), h] = <u[row_p, h, :], v[col_p, h, :]>.
  * AttIGCN.masked_mm (model.py:4246-4255) with u = x_q (dst rows),

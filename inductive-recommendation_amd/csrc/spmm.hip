@@ -98,22 +98,30 @@ struct W_ValEid {  // rhs by edge id, edge id = edge_id[p] (multigraph / reverse
     const int64_t *eid;
     __device__ __forceinline__ float operator()(int64_t p, int, int) const { return val[ld_stream(eid + p)]; }
 };
+// Key of an edge for the dropout draw: its (row, column) in the frame the
+// mask was drawn for (a coalesced graph has one edge per pair), so the reverse
+// graph regenerates the forward's mask from its own (column, row) without
+// reading an edge-id permutation.
+__device__ __forceinline__ uint64_t edge_key(uint32_t r, uint32_t c) {
+    return mix64(((uint64_t)r << 32) | c);
+}
+
 // Row / column scaled weights with fused dropout (igr_spmm_scaled_f32):
 //   w = rs[r] * cs[c], then dropped (0) or divided by keep, the mask drawn from
-//   uniform24(seed, offset, edge id) so the reverse graph regenerates the
-//   forward's mask exactly.
+//   uniform24(seed, offset, edge_key(forward row, forward column)); swap = this
+//   graph is the reverse of the mask's frame.
 struct W_Scaled {
     const float *rs, *cs;
-    const int64_t *eid;
     float keep;
     uint64_t seed, offset;
-    __device__ __forceinline__ float operator()(int64_t p, int c, int r) const {
+    int swap;
+    __device__ __forceinline__ float operator()(int64_t, int c, int r) const {
         float w = rs ? rs[r] : 1.f;
         if (cs) w *= cs[c];
         if (keep < 1.f) {
-            const int64_t e = eid ? ld_stream(eid + p) : p;
+            const uint64_t k = swap ? edge_key((uint32_t)c, (uint32_t)r) : edge_key((uint32_t)r, (uint32_t)c);
             // random_tensor = keep + U; mask = floor(random_tensor) (model.py:4019-4021)
-            w = (floorf(keep + uniform24(seed, offset, (uint64_t)e)) != 0.f) ? w / keep : 0.f;
+            w = (floorf(keep + uniform24(seed, offset, k)) != 0.f) ? w / keep : 0.f;
         }
         return w;
     }
@@ -382,10 +390,15 @@ static int run_spmm(const char *fn, const igr_csr *g, int32_t d, const float *x,
     return launch_status(fn);
 }
 
-// The uniforms W_Scaled draws for edge ids 0..n-1 (tests / explicit-values path).
-__global__ void uniforms_kernel(int64_t n, uint64_t seed, uint64_t offset, float *__restrict__ out) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = uniform24(seed, offset, (uint64_t)i);
+// The uniforms W_Scaled draws, per CSR position of g (tests / explicit-values path).
+__global__ void uniforms_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                                uint64_t seed, uint64_t offset, int swap, float *__restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows) return;
+    for (int64_t p = row_ptr[r]; p < row_ptr[r + 1]; ++p) {
+        const uint32_t c = (uint32_t)col[p];
+        out[p] = uniform24(seed, offset, swap ? edge_key(c, (uint32_t)r) : edge_key((uint32_t)r, c));
+    }
 }
 
 }  // namespace igr
@@ -406,24 +419,27 @@ extern "C" int igr_spmm_f32(const igr_csr *g, int32_t d, const float *x, int64_t
 
 extern "C" int igr_spmm_scaled_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx,
                                    const float *row_scale, const float *col_scale, float keep, uint64_t seed,
-                                   uint64_t offset, float *y, int64_t ldy, const igr_epilogue *epi,
-                                   float *workspace, void *stream) {
+                                   uint64_t offset, int32_t transposed, float *y, int64_t ldy,
+                                   const igr_epilogue *epi, float *workspace, void *stream) {
     return guarded("igr_spmm_scaled_f32", [&]() -> int {
         const char *fn = "igr_spmm_scaled_f32";
         if (!g) return arg_error(fn, "graph is NULL");
         if (!(keep > 0.f && keep <= 1.f)) return arg_error(fn, "keep must be in (0, 1]");
-        return run_spmm(fn, g, d, x, ldx, W_Scaled{row_scale, col_scale, g->edge_id, keep, seed, offset}, y, ldy,
-                        epi, workspace, stream);
+        if (keep < 1.f && (g->n_rows > 4294967295LL || g->n_cols > 4294967295LL))
+            return arg_error(fn, "dropout keys need row / column ids below 2^32");
+        return run_spmm(fn, g, d, x, ldx, W_Scaled{row_scale, col_scale, keep, seed, offset, transposed ? 1 : 0}, y,
+                        ldy, epi, workspace, stream);
     });
 }
 
-extern "C" int igr_dropout_uniforms(int64_t n, uint64_t seed, uint64_t offset, float *out, void *stream) {
+extern "C" int igr_dropout_uniforms(const igr_csr *g, uint64_t seed, uint64_t offset, int32_t transposed, float *out,
+                                    void *stream) {
     return guarded("igr_dropout_uniforms", [&]() -> int {
-        if (n <= 0) return IGR_OK;
+        if (!g || !out) return arg_error("igr_dropout_uniforms", "graph / out NULL");
+        if (g->n_rows <= 0 || g->nnz <= 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-        int64_t blocks = (n + 255) / 256;
-        if (blocks > 16384) blocks = 16384;
-        hipLaunchKernelGGL(uniforms_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n, seed, offset, out);
+        hipLaunchKernelGGL(uniforms_kernel, dim3((unsigned)((g->n_rows + 255) / 256)), dim3(256), 0, st, g->n_rows,
+                           g->row_ptr, g->col_idx, seed, offset, transposed ? 1 : 0, out);
         return launch_status("igr_dropout_uniforms");
     });
 }

@@ -53,7 +53,7 @@ SIGNATURES = {
     'igr_plan_fill': (ctypes.c_int, [c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'igr_spmm_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, _P(IgrEpilogue), c_vp, c_vp]),
     'igr_spmm_scaled_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_vp, c_f32, ctypes.c_uint64,
-                                           ctypes.c_uint64, c_vp, c_i64, _P(IgrEpilogue), c_vp, c_vp]),
+                                           ctypes.c_uint64, c_i32, c_vp, c_i64, _P(IgrEpilogue), c_vp, c_vp]),
     'igr_spmm_rows_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                          c_i64, c_f32, c_vp, c_i64, c_vp]),
     'igr_spmm_push_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_f32, c_i32, c_vp,
@@ -65,7 +65,7 @@ SIGNATURES = {
     'igr_rowset_clear': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     'igr_mask_scores_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     'igr_topk_f32': (ctypes.c_int, [c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),
-    'igr_dropout_uniforms': (ctypes.c_int, [c_i64, ctypes.c_uint64, ctypes.c_uint64, c_vp, c_vp]),
+    'igr_dropout_uniforms': (ctypes.c_int, [_P(IgrCsr), ctypes.c_uint64, ctypes.c_uint64, c_i32, c_vp, c_vp]),
     'igr_sddmm_dot_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     'igr_segment_reduce_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i32, c_vp, c_vp]),
     'igr_att_softmax_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),

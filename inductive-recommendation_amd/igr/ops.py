@@ -104,16 +104,18 @@ def spmm(g: Graph, x, rhs=None, out=None, epi=None):
 class ScaledWeights:
     """Edge weights w = row_scale[r] * col_scale[c], dropout fused in-kernel with
     keep probability `keep` and a counter-based mask keyed by (seed, offset,
-    edge id) - igr_spmm_scaled_f32.  For a graph whose values are row-constant
-    (the IGCN feature graph) this replaces the per-edge value array, the rand
-    tensor and the dropout pass."""
+    the edge's (row, column) in the frame it was drawn for) -
+    igr_spmm_scaled_f32.  For a graph whose values are row-constant (the IGCN
+    feature graph) this replaces the per-edge value array, the rand tensor and
+    the dropout pass.  `swap`: applied to the reverse of that frame."""
 
-    def __init__(self, row_scale=None, col_scale=None, keep=1.0, seed=0, offset=0):
+    def __init__(self, row_scale=None, col_scale=None, keep=1.0, seed=0, offset=0, swap=False):
         self.row_scale, self.col_scale = row_scale, col_scale
         self.keep, self.seed, self.offset = float(keep), int(seed), int(offset)
+        self.swap = bool(swap)
 
     def transposed(self):
-        return ScaledWeights(self.col_scale, self.row_scale, self.keep, self.seed, self.offset)
+        return ScaledWeights(self.col_scale, self.row_scale, self.keep, self.seed, self.offset, not self.swap)
 
 
 def spmm_scaled(g: Graph, x, w: ScaledWeights, out=None, epi=None):
@@ -130,16 +132,16 @@ def spmm_scaled(g: Graph, x, w: ScaledWeights, out=None, epi=None):
     if out is None:
         out = torch.empty(g.n_rows, d, dtype=torch.float32, device=x.device)
     L.call('igr_spmm_scaled_f32', ctypes.byref(g.csr), d, _p(x), ldx, _p(w.row_scale), _p(w.col_scale), w.keep,
-           ctypes.c_uint64(w.seed & (2 ** 64 - 1)), ctypes.c_uint64(w.offset & (2 ** 64 - 1)), _p(out),
+           ctypes.c_uint64(w.seed & (2 ** 64 - 1)), ctypes.c_uint64(w.offset & (2 ** 64 - 1)), int(w.swap), _p(out),
            out.stride(0), None if epi is None else ctypes.byref(epi), _p(g.workspace(d)), _stream())
     return out
 
 
-def dropout_uniforms(n, seed, offset, device):
-    """The uniforms ScaledWeights' dropout draws for edge ids 0..n-1."""
-    out = torch.empty(n, dtype=torch.float32, device=device)
-    L.call('igr_dropout_uniforms', n, ctypes.c_uint64(seed & (2 ** 64 - 1)), ctypes.c_uint64(offset & (2 ** 64 - 1)),
-           _p(out), _stream())
+def dropout_uniforms(g: Graph, seed, offset, swap=False):
+    """The uniforms ScaledWeights(seed, offset, swap)'s dropout draws on g, per CSR position."""
+    out = torch.empty(g.nnz, dtype=torch.float32, device=g.device)
+    L.call('igr_dropout_uniforms', ctypes.byref(g.csr), ctypes.c_uint64(seed & (2 ** 64 - 1)),
+           ctypes.c_uint64(offset & (2 ** 64 - 1)), int(bool(swap)), _p(out), _stream())
     return out
 
 
@@ -172,7 +174,7 @@ def _prescale(fw):
 def _feat_spmm_rev(feat, dx, fw, prescaled):
     """demb = F_w^T dx; `prescaled` means dx already carries fw's row scale."""
     if prescaled:
-        return spmm_scaled(feat.reverse(), dx, ScaledWeights(None, None, fw.keep, fw.seed, fw.offset))
+        return spmm_scaled(feat.reverse(), dx, ScaledWeights(None, None, fw.keep, fw.seed, fw.offset, not fw.swap))
     return _feat_spmm(feat, dx, fw, reverse=True)
 
 

@@ -50,8 +50,9 @@ def main():
     cases = {
         'forward': lambda: ops.spmm_scaled(g, emb, ops.ScaledWeights(rv), out=out_f),
         'forward_dropout': lambda: ops.spmm_scaled(g, emb, ops.ScaledWeights(rv, None, 0.7, 5, 1), out=out_f),
-        'reverse_col_scale': lambda: ops.spmm_scaled(gr, dx, ops.ScaledWeights(None, rv, 0.7, 5, 1), out=out_r),
-        'reverse_prescaled': lambda: ops.spmm_scaled(gr, dx, ops.ScaledWeights(None, None, 0.7, 5, 1), out=out_r),
+        'reverse_col_scale': lambda: ops.spmm_scaled(gr, dx, ops.ScaledWeights(None, rv, 0.7, 5, 1, True), out=out_r),
+        'reverse_prescaled': lambda: ops.spmm_scaled(gr, dx, ops.ScaledWeights(None, None, 0.7, 5, 1, True),
+                                                     out=out_r),
     }
     res = {}
     for name, fn in cases.items():

@@ -183,8 +183,8 @@ class BasicTrainer:
             if banned_items is not None:
                 scores[:, torch.as_tensor(banned_items, device=self.device)] = -np.inf
             _, items = ops.topk(scores, kmax, values=False)
-            rec.append(items.cpu().numpy())
-        return np.concatenate(rec, axis=0)
+            rec.append(items)  # stays on the device: one copy (and sync) per eval, not per batch
+        return torch.cat(rec).cpu().numpy()
 
     def eval(self, val_or_test, banned_items=None):
         """trainer.py:146-210; returns (result string, metrics).

@@ -139,3 +139,53 @@ def test_reverse_graph_edge_ids():
     rrows = np.repeat(np.arange(30), np.diff(rh['row_ptr']))
     np.testing.assert_array_equal(src[rh['edge_id']], rrows)
     np.testing.assert_array_equal(dst[rh['edge_id']], rh['col_idx'])
+
+
+def _refused(name, *args, match=None):
+    """The call must fail argument validation (before any device work) with IGR_ERR_ARG."""
+    rc = getattr(_lib.lib(), name)(*args)
+    assert rc == 1, (name, rc)
+    if match:
+        msg = _lib.lib().igr_last_error().decode()
+        assert re.search(match, msg), msg
+
+
+def test_new_entry_points_validate_arguments():
+    """Argument checks of the batch-row, pull, top-k, split-K GEMM, BPR and fused-dropout
+    entry points run on the host: wrong shapes are refused with IGR_ERR_ARG and a message."""
+    F = ctypes.c_void_p(0x10000)  # 16-B aligned stand-in device pointer, never dereferenced here
+    rp, ci, _, eid = G.csr_from_coo(np.array([0, 1, 1]), np.array([1, 0, 2]), 2, 3, dedup=False)
+    rect = G.Graph(rp, ci, 2, 3, device='cpu')  # 2 x 3
+    multi = G.Graph(rp, ci, 2, 3, device='cpu', edge_id=eid[::-1].copy())
+    st = None
+    # top-k: k in [1, 1024] and <= n_cols; ld >= n_cols
+    _refused('igr_topk_f32', 2, 5, F, 5, 6, F, F, st, match='k larger')
+    _refused('igr_topk_f32', 2, 5, F, 5, 0, F, F, st, match=r'\[1, 1024\]')
+    _refused('igr_topk_f32', 2, 5000, F, 5000, 2000, F, F, st, match=r'\[1, 1024\]')
+    _refused('igr_topk_f32', 2, 5, F, 4, 2, F, F, st, match='ld')
+    _refused('igr_mask_scores_f32', 2, None, None, F, 5, st, match='NULL')
+    # GEMM: sizes / leading dims; the split-K workspace is asked for only where it is used
+    _refused('igr_gemm_f32', -1, 4, 4, F, 4, 0, F, 4, 0, None, F, 4, None, 0, st, match='negative')
+    _refused('igr_gemm_f32', 8, 8, 8, F, 8, 0, F, 8, 0, None, F, 4, None, 0, st, match='ldc')
+    assert _lib.lib().igr_gemm_workspace_size(256, 64, 9750) > 0  # weight gradient: split K
+    assert _lib.lib().igr_gemm_workspace_size(100000, 64, 64) == 0  # tall: no split
+    # row-restricted SpMM / push / pull
+    _refused('igr_spmm_rows_f32', ctypes.byref(rect.csr), 48, F, 4, F, 48, None, None, 0, None, 0, 1.0, F, 48, st,
+             match='d must be')
+    _refused('igr_spmm_rows_f32', ctypes.byref(multi.csr), 64, F, 4, F, 64, F, None, 0, None, 0, 1.0, F, 64, st,
+             match='edge_id')
+    tall = G.Graph(np.array([0, 1, 2, 3]), np.array([0, 1, 0], np.int32), 3, 2, device='cpu')  # 3 x 2
+    _refused('igr_spmm_push_f32', ctypes.byref(tall.csr), 64, F, 4, F, 64, None, 1.0, 1, F, 64, st, match='square')
+    _refused('igr_spmm_pull_marked_f32', ctypes.byref(rect.csr), 64, None, F, F, F, 64, None, 1.0, 0, F, 64, st,
+             match='NULL')
+    _refused('igr_spmm_pull_marked_f32', ctypes.byref(multi.csr), 64, F, F, F, F, 64, F, 1.0, 0, F, 64, st,
+             match='edge_id')
+    _refused('igr_rowset_mark', 4, F, None, F, F, st, match='NULL')
+    _refused('igr_rowset_sum_f32', 4, 64, F, F, F, 32, 1.0, F, 64, st, match='leading')
+    # fused BPR: the LDS dw reduction bounds d; fused dropout: keep in (0, 1]
+    _refused('igr_bpr_fwd_bwd_f32', 4, 2000, F, F, F, 0, 0, F, 2000, F, None, None, 1.0, 0.0, None, None, None, 0,
+             F, st, match='1024')
+    for keep in (0.0, 1.5):
+        _refused('igr_spmm_scaled_f32', ctypes.byref(rect.csr), 64, F, 64, None, None, keep, 1, 0, 0, F, 64, None,
+                 F, st, match='keep')
+    _refused('igr_dropout_uniforms', None, 1, 0, 0, F, st, match='NULL')

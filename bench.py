@@ -117,6 +117,8 @@ def main():
     ap.add_argument('--cpu-sample-edges', type=int, default=20_000_000)
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'))
     ap.add_argument('--item-tiles', default='auto', help="source tiles of the item-side SpMM ('auto' or an int)")
+    ap.add_argument('--replicate', default='auto', choices=['auto', 'items', 'users'],
+                    help='side replicated on every rank (auto: the smaller one); the other is cut into ranges')
     ap.add_argument('--dist-backend', default='nccl', help="'nccl' (= RCCL on ROCm); 'gloo' only for rehearsals")
     ap.add_argument('--one-device', action='store_true',
                     help='map every rank to cuda:0 (multi-rank rehearsal on a one-GPU box, with --dist-backend gloo)')
@@ -137,14 +139,18 @@ def main():
 
     from igr import ops
     from igr.dataset import synthetic_pairs
-    from igr.dist import BipartiteShard
+    from igr.dist import BipartiteShard, sharded_side
 
     U, I, E, d = args.n_users, args.n_items, args.n_edges, args.d
     t0 = time.time()
     log(f'rank {rank}/{world}: drawing {E} interactions (U={U}, I={I}, {args.item_dist}, seed {args.seed})')
     pairs = synthetic_pairs(U, I, E, args.seed, args.item_dist)
-    log(f'building shard (C++ CSR build) ... {time.time() - t0:.1f}s')
-    shard = BipartiteShard(pairs, U, I, rank, world, dev, d=d, item_tiles=args.item_tiles)
+    side = sharded_side(U, I, args.replicate)
+    SU, SI = (U, I) if side == 'users' else (I, U)  # the shard cuts its first side into ranges
+    if side == 'items':
+        pairs = np.ascontiguousarray(pairs[:, ::-1])
+    log(f'building shard (C++ CSR build; {side} sharded) ... {time.time() - t0:.1f}s')
+    shard = BipartiteShard(pairs, SU, SI, rank, world, dev, d=d, item_tiles=args.item_tiles)
     del pairs
     nu = shard.u1 - shard.u0
     log(f'shard users [{shard.u0}, {shard.u1}) local nnz {shard.local_nnz} '
@@ -152,11 +158,11 @@ def main():
         f'... {time.time() - t0:.1f}s')
 
     g = torch.Generator(device=dev).manual_seed(2 + args.seed)
-    x_items = torch.randn(I, d, generator=g, device=dev) * 0.1
+    x_items = torch.randn(SI, d, generator=g, device=dev) * 0.1  # the replicated side
     g.manual_seed(3 + args.seed + rank)
     x_users = torch.randn(nu, d, generator=g, device=dev) * 0.1
     y_users = torch.empty(nu, d, device=dev)
-    y_items = torch.empty(I, d, device=dev)
+    y_items = torch.empty(SI, d, device=dev)
     stream = torch.cuda.current_stream()
     launches = shard.launches()
     launch_bytes = [spmm_bytes(nnz, n_rows, d) for _, _, _, n_rows, nnz in launches]
@@ -223,7 +229,8 @@ def main():
             'config': {'workload': f'synthetic bipartite {U} users x {I} items, {E} {args.item_dist} draws, '
                                    f'd={d}: one SpMM layer Y = D^-1/2 A D^-1/2 X over all {total_nnz} edges',
                        'n_users': U, 'n_items': I, 'n_draws': E, 'nnz': total_nnz, 'd': d,
-                       'parallelism': f'user-range shards x{world}, item block replicated, RCCL all-reduce',
+                       'parallelism': (f'{side[:-1]}-range shards x{world}, '
+                                       f'{"item" if side == "users" else "user"} block replicated, RCCL all-reduce'),
                        'item_source_tiles': shard.item_tiles, 'launches_per_step': nl},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic,

@@ -17,7 +17,10 @@ One propagation layer Y = A X of the symmetric-normalised bipartite graph:
 The all-reduce is issued right after the item-side SpMM and overlaps the
 user-side SpMM (RCCL runs on its own stream).  The collective moves only
 I x d floats per layer (256 MB at I = 1M, d = 64), never the user block.
-The smaller side should be the replicated one; `replicate` picks it.
+The smaller side should be the replicated one: the layer is symmetric in the
+two sides, so a caller whose items outnumber its users passes the pairs with
+their columns swapped (then 'users' below means the sharded side) -
+`sharded_side` / bench.py --replicate.
 """
 import numpy as np
 import torch
@@ -27,6 +30,16 @@ from . import ops
 from .graph import Graph, TiledGraph, csr_from_coo, sym_norm_values
 
 MALL_BYTES = 256 << 20  # MI355X Infinity Cache
+
+
+def sharded_side(n_users, n_items, replicate='auto'):
+    """'users' or 'items': the side a BipartiteShard cuts into ranges (the other is
+    replicated); 'auto' replicates the smaller side."""
+    if replicate == 'auto':
+        return 'users' if n_users >= n_items else 'items'
+    if replicate not in ('items', 'users'):
+        raise ValueError(f"replicate must be 'auto', 'items' or 'users', got {replicate!r}")
+    return 'users' if replicate == 'items' else 'items'
 
 
 def balanced_ranges(degree, world):

@@ -283,3 +283,29 @@ def test_sharded_batch_rows_match_unsharded(L):
         np.testing.assert_allclose(rep_b, np.concatenate([rep[u0 + users], rep[U + items]]), **tol)
         np.testing.assert_allclose(grad_k[:nk], grad[u0:u1], **tol)
         np.testing.assert_allclose(grad_k[nk:], grad[U:], **tol)
+
+
+def test_sharded_side_replicates_the_smaller_side():
+    from igr.dist import sharded_side
+    assert sharded_side(10_000_000, 1_000_000) == 'users'  # items replicated
+    assert sharded_side(50_000, 2_900_000) == 'items'  # Amazon-Books-like: users replicated
+    assert sharded_side(5, 10, 'items') == 'users' and sharded_side(10, 5, 'users') == 'items'
+    with pytest.raises(ValueError):
+        sharded_side(1, 1, 'both')
+
+
+def test_swapped_sides_layer_matches_oracle():
+    """With items outnumbering users the pairs are passed column-swapped (items sharded,
+    users replicated); one layer then equals A x restricted to each side."""
+    rng = np.random.default_rng(9)
+    U, I, d = 30, 200, 8
+    pairs = np.stack([rng.integers(0, U, 1500), rng.integers(0, I, 1500)], 1)
+    sw = np.ascontiguousarray(pairs[:, ::-1])
+    sh = BipartiteShard(sw, I, U, 0, 1, 'cpu')  # items are the cut side
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(U + I, d, generator=g)
+    y_items, y_users = sh.layer(x[U:].contiguous(), x[:U].contiguous(), spmm=oracle_spmm)
+    A = O.norm_adj(U, I, pairs)
+    ref = O.spmm(A, x.numpy())
+    np.testing.assert_allclose(y_users.numpy(), ref[:U], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(y_items.numpy(), ref[U:], rtol=1e-5, atol=1e-6)

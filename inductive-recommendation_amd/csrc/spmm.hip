@@ -284,10 +284,22 @@ __global__ __launch_bounds__(256) void spmm_combine(const int32_t *__restrict__ 
     const int sub = threadIdx.x - slot * LPR;
     const int64_t i = blockIdx.x;
     if (i >= n_split) return;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t c = split_ptr[i] + slot; c < split_ptr[i + 1]; c += S)
-        acc = f4_add(acc, *reinterpret_cast<const float4 *>(ws + c * D + sub * 4));
-    red[slot][sub] = acc;
+    // 8 independent partial sums per slot keep 8 loads in flight (a hub row's
+    // slots each walk ~100+ partials); combined in a fixed tree: deterministic
+    constexpr int V = 8;
+    float4 a[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t c = split_ptr[i] + slot;
+    const int64_t e = split_ptr[i + 1];
+    for (; c + (V - 1) * S < e; c += V * S) {
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+            a[j] = f4_add(a[j], *reinterpret_cast<const float4 *>(ws + (c + j * S) * D + sub * 4));
+    }
+    for (; c < e; c += S) a[0] = f4_add(a[0], *reinterpret_cast<const float4 *>(ws + c * D + sub * 4));
+    red[slot][sub] = f4_add(f4_add(f4_add(a[0], a[1]), f4_add(a[2], a[3])),
+                            f4_add(f4_add(a[4], a[5]), f4_add(a[6], a[7])));
     __syncthreads();
 #pragma unroll
     for (int w = S / 2; w >= 1; w >>= 1) {

@@ -173,6 +173,30 @@ __device__ __forceinline__ float4 gather_block(float4 acc, int cl, float vl, int
     return acc;
 }
 
+// One round of NB (col, val) blocks of LPR edges each (n <= NB*LPR edges):
+// edge j lives in block j / LPR, lane gbase + j % LPR - both compile-time, so
+// all n row gathers are issued before their FMAs (narrow rows, d = 32, where a
+// single LPR-edge block would leave only 8 gathers in flight per group).
+template <int NB, int LPR>
+__device__ __forceinline__ float4 gather_round(float4 acc, const int (&cl)[NB], const float (&vl)[NB], int gbase,
+                                               int n, const float *__restrict__ xs, int64_t ldx) {
+    constexpr int BE = NB * LPR;
+    float4 xv[BE];
+    float wv[BE];
+#pragma unroll
+    for (int j = 0; j < BE; ++j) {
+        if (j < n) {
+            const int c = shfl_i(cl[j / LPR], gbase + j % LPR);
+            wv[j] = shfl_f(vl[j / LPR], gbase + j % LPR);
+            xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < BE; ++j)
+        if (j < n) acc = f4_fma(wv[j], xv[j], acc);
+    return acc;
+}
+
 template <int D, class W>
 __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col, W wfn,
@@ -241,6 +265,48 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
     const int64_t b = row_ptr[r], e = row_ptr[r + 1];
     const int gbase = grp * LPR;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int NB = LPR >= 16 ? 1 : 16 / LPR;  // (col, val) blocks per round
+    if constexpr (NB > 1) {
+        constexpr int BE = NB * LPR;
+        int64_t base = b;
+        int n = (int)min((int64_t)BE, e - base);
+        int cl[NB];
+        float vl[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            cl[k] = 0;
+            vl[k] = 0.f;
+            if (k * LPR + sub < n) {
+                cl[k] = ld_stream(col + base + k * LPR + sub);
+                vl[k] = wfn(base + k * LPR + sub, cl[k], r);
+            }
+        }
+        while (n > 0) {
+            const int64_t nb = base + BE;
+            const int nn = (int)min((int64_t)BE, e - nb);
+            int cl2[NB];
+            float vl2[NB];
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {  // next round's pairs, under this round's gathers
+                cl2[k] = 0;
+                vl2[k] = 0.f;
+                if (k * LPR + sub < nn) {
+                    cl2[k] = ld_stream(col + nb + k * LPR + sub);
+                    vl2[k] = wfn(nb + k * LPR + sub, cl2[k], r);
+                }
+            }
+            acc = gather_round<NB, LPR>(acc, cl, vl, gbase, n, xs, ldx);
+            base = nb;
+            n = nn;
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                cl[k] = cl2[k];
+                vl[k] = vl2[k];
+            }
+        }
+        store_row4(epi, r, sub * 4, acc);
+        return;
+    }
     int64_t base = b;
     int n = (int)min((int64_t)LPR, e - base);
     int cl = 0;

@@ -217,6 +217,213 @@ __global__ __launch_bounds__(256) void att_softmax_bwd_kernel(
     }
 }
 
+// ---------------------------------------------------------------- grouped softmax (H heads, 16 lanes per row)
+#ifndef IGR_SOFTMAX_R
+#define IGR_SOFTMAX_R 4  // register-cached edges per lane at H <= 4 (H = 8: half); swept 2/4/8/16 on MI355X
+#endif
+// The feature graph's rows are short (a user row ~20 edges, an item row ~200):
+// a wave per row leaves most lanes idle and pays a 64-lane reduction per head
+// three times.  Here 16 lanes take a row (4 rows per wave); each lane keeps the
+// alpha rows of its first R edges in registers (one read of alpha; edges past
+// 16R, if any, are re-read), the exps are computed once, and the row max / sum
+// are 4-step xor reductions inside the 16 lanes.
+template <int H>
+__device__ __forceinline__ void load_heads(const float *__restrict__ alpha, int64_t ed, float (&a)[H]) {
+    if constexpr (H % 4 == 0) {
+#pragma unroll
+        for (int q = 0; q < H / 4; ++q) {
+            const float4 v = *reinterpret_cast<const float4 *>(alpha + ed * H + 4 * q);
+            a[4 * q] = v.x;
+            a[4 * q + 1] = v.y;
+            a[4 * q + 2] = v.z;
+            a[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < H; ++j) a[j] = alpha[ed * H + j];
+    }
+}
+
+__device__ __forceinline__ float g16_max(float v) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ float g16_sum(float v) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int H, int R>
+__global__ __launch_bounds__(256) void att_softmax_g16_kernel(
+    int64_t n_rows, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
+    const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d, float *__restrict__ w,
+    float *__restrict__ row_max, float *__restrict__ row_sum) {
+    const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int sub = threadIdx.x & 15;
+    const bool live = r < n_rows;  // every lane stays for the group shuffles
+    const int64_t b = live ? row_ptr[r] : 0, e = live ? row_ptr[r + 1] : 0;
+    float a[R][H];
+    bool k[R];
+    float m[H], sm[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) m[j] = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const int64_t p = b + sub + 16 * t;
+        k[t] = false;
+        if (p < e) {
+            const int64_t ed = eid ? eid[p] : p;
+            k[t] = kept(keep, ed);
+            if (k[t]) {
+                load_heads<H>(alpha, ed, a[t]);
+#pragma unroll
+                for (int j = 0; j < H; ++j) m[j] = fmaxf(m[j], a[t][j]);
+            }
+        }
+    }
+    for (int64_t p = b + sub + 16 * R; p < e; p += 16) {  // past the register cache
+        const int64_t ed = eid ? eid[p] : p;
+        if (!kept(keep, ed)) continue;
+        float x[H];
+        load_heads<H>(alpha, ed, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) m[j] = fmaxf(m[j], x[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        m[j] = g16_max(m[j]);
+        sm[j] = 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+        if (k[t]) {
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                a[t][j] = att_exp(a[t][j], m[j], sqrt_d);
+                sm[j] += a[t][j];
+            }
+        }
+    for (int64_t p = b + sub + 16 * R; p < e; p += 16) {
+        const int64_t ed = eid ? eid[p] : p;
+        if (!kept(keep, ed)) continue;
+        float x[H];
+        load_heads<H>(alpha, ed, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) sm[j] += att_exp(x[j], m[j], sqrt_d);
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) sm[j] = g16_sum(sm[j]);
+    if (!live || b == e) return;
+    if (sub == 0) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            if (row_max) row_max[r * H + j] = m[j];
+            if (row_sum) row_sum[r * H + j] = sm[j];
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const int64_t p = b + sub + 16 * t;
+        if (p < e) {
+            const int64_t ed = eid ? eid[p] : p;
+            float acc = 0.f;
+            if (k[t]) {
+#pragma unroll
+                for (int j = 0; j < H; ++j) acc += a[t][j] / sm[j];
+                acc /= (float)H;
+            }
+            w[ed] = acc;
+        }
+    }
+    for (int64_t p = b + sub + 16 * R; p < e; p += 16) {
+        const int64_t ed = eid ? eid[p] : p;
+        if (!kept(keep, ed)) {
+            w[ed] = 0.f;
+            continue;
+        }
+        float x[H];
+        load_heads<H>(alpha, ed, x);
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < H; ++j) acc += att_exp(x[j], m[j], sqrt_d) / sm[j];
+        w[ed] = acc / (float)H;
+    }
+}
+
+template <int H, int R>
+__global__ __launch_bounds__(256) void att_softmax_bwd_g16_kernel(
+    int64_t n_rows, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
+    const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d, const float *__restrict__ row_max,
+    const float *__restrict__ row_sum, const float *__restrict__ dw, float *__restrict__ dalpha) {
+    const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int sub = threadIdx.x & 15;
+    const bool live = r < n_rows;
+    const int64_t b = live ? row_ptr[r] : 0, e = live ? row_ptr[r + 1] : 0;
+    float m[H], s[H], S[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        m[j] = live && b < e ? row_max[r * H + j] : 0.f;
+        s[j] = live && b < e ? row_sum[r * H + j] : 1.f;
+        S[j] = 0.f;
+    }
+    const float inv_h = 1.f / (float)H;
+    float a[R][H], g[R];
+    bool k[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const int64_t p = b + sub + 16 * t;
+        k[t] = false;
+        g[t] = 0.f;
+        if (p < e) {
+            const int64_t ed = eid ? eid[p] : p;
+            g[t] = dw[ed] * inv_h;
+            k[t] = kept(keep, ed);
+            if (k[t]) {
+                load_heads<H>(alpha, ed, a[t]);
+#pragma unroll
+                for (int j = 0; j < H; ++j) {
+                    a[t][j] = att_exp(a[t][j], m[j], sqrt_d) / s[j];
+                    S[j] += a[t][j] * g[t];
+                }
+            }
+        }
+    }
+    for (int64_t p = b + sub + 16 * R; p < e; p += 16) {
+        const int64_t ed = eid ? eid[p] : p;
+        if (!kept(keep, ed)) continue;
+        const float gg = dw[ed] * inv_h;
+        float x[H];
+        load_heads<H>(alpha, ed, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) S[j] += att_exp(x[j], m[j], sqrt_d) / s[j] * gg;
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) S[j] = g16_sum(S[j]);
+    if (!live || b == e) return;
+    const float c = sqrt_d * 10.f;
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const int64_t p = b + sub + 16 * t;
+        if (p < e) {
+            const int64_t ed = eid ? eid[p] : p;
+#pragma unroll
+            for (int j = 0; j < H; ++j) dalpha[ed * H + j] = k[t] ? a[t][j] * (g[t] - S[j]) / c : 0.f;
+        }
+    }
+    for (int64_t p = b + sub + 16 * R; p < e; p += 16) {
+        const int64_t ed = eid ? eid[p] : p;
+        const bool kk = kept(keep, ed);
+        const float gg = dw[ed] * inv_h;
+        float x[H];
+        if (kk) load_heads<H>(alpha, ed, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) dalpha[ed * H + j] = kk ? att_exp(x[j], m[j], sqrt_d) / s[j] * (gg - S[j]) / c : 0.f;
+    }
+}
+
 // ---------------------------------------------------------------- value kernels
 __global__ void edge_dropout_kernel(int64_t n, const float *__restrict__ val,
                                     const float *__restrict__ rand, float keep,
@@ -306,9 +513,20 @@ extern "C" int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alp
         if (!g || h <= 0 || h > kMaxHeads) return arg_error(fn, "h must be in [1, 8]");
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-        hipLaunchKernelGGL(att_softmax_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0,
-                           st, g->n_rows, h, g->row_ptr, g->edge_id, alpha, keep, sqrt_d, w, row_max,
-                           row_sum);
+        const dim3 g16((unsigned)((g->n_rows + 15) / 16));
+        const bool vec = (reinterpret_cast<uintptr_t>(alpha) & 15u) == 0;
+#define IGR_SM(HH, RR)                                                                                       \
+    hipLaunchKernelGGL((att_softmax_g16_kernel<HH, RR>), g16, dim3(256), 0, st, g->n_rows, g->row_ptr, g->edge_id, \
+                       alpha, keep, sqrt_d, w, row_max, row_sum)
+        if (h == 1) IGR_SM(1, IGR_SOFTMAX_R);
+        else if (h == 2) IGR_SM(2, IGR_SOFTMAX_R);
+        else if (h == 4 && vec) IGR_SM(4, IGR_SOFTMAX_R);
+        else if (h == 8 && vec) IGR_SM(8, (IGR_SOFTMAX_R + 1) / 2);
+        else
+            hipLaunchKernelGGL(att_softmax_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0,
+                               st, g->n_rows, h, g->row_ptr, g->edge_id, alpha, keep, sqrt_d, w, row_max,
+                               row_sum);
+#undef IGR_SM
         return launch_status(fn);
     });
 }
@@ -322,9 +540,20 @@ extern "C" int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float 
         if (!row_max || !row_sum) return arg_error(fn, "row_max / row_sum required");
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-        hipLaunchKernelGGL(att_softmax_bwd_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256),
-                           0, st, g->n_rows, h, g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max,
-                           row_sum, dw, dalpha);
+        const dim3 g16((unsigned)((g->n_rows + 15) / 16));
+        const bool vec = (reinterpret_cast<uintptr_t>(alpha) & 15u) == 0;
+#define IGR_SMB(HH, RR)                                                                                           \
+    hipLaunchKernelGGL((att_softmax_bwd_g16_kernel<HH, RR>), g16, dim3(256), 0, st, g->n_rows, g->row_ptr,         \
+                       g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha)
+        if (h == 1) IGR_SMB(1, IGR_SOFTMAX_R);
+        else if (h == 2) IGR_SMB(2, IGR_SOFTMAX_R);
+        else if (h == 4 && vec) IGR_SMB(4, IGR_SOFTMAX_R);
+        else if (h == 8 && vec) IGR_SMB(8, (IGR_SOFTMAX_R + 1) / 2);
+        else
+            hipLaunchKernelGGL(att_softmax_bwd_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256),
+                               0, st, g->n_rows, h, g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max,
+                               row_sum, dw, dalpha);
+#undef IGR_SMB
         return launch_status(fn);
     });
 }

@@ -58,7 +58,12 @@ def _rows(t):
 # ------------------------------------------------------------------ raw ops
 
 def epilogue(alpha=1.0, beta=0.0, add=None, acc=None, acc_mode=0, acc_div=1.0, skip_y=False, row_scale=None):
+    """struct igr_epilogue for spmm / spmm_scaled.  The struct holds raw device
+    pointers, so it also keeps the tensors alive (an inline temporary such as
+    `epilogue(add=x * 2)` would otherwise be freed - and its memory reused by
+    the caching allocator - before the kernel reads it)."""
     e = L.IgrEpilogue()
+    e._refs = (add, acc, row_scale)
     if row_scale is not None:
         _f32(row_scale)
         e.row_scale = row_scale.data_ptr()

@@ -33,16 +33,27 @@ __global__ __launch_bounds__(256) void sddmm_dot_kernel(
     const int hs = d / 4;  // lanes per head (power of two, checked by the host)
     const float4 uq = *reinterpret_cast<const float4 *>(u + r * ld_u + sub * 4);
     const int64_t b = row_ptr[r], e = row_ptr[r + 1];
-    for (int64_t base = b; base < e; base += EPW) {
-        const int64_t p = base + eg;
-        const bool ok = p < e;
-        float4 vk = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ok) vk = *reinterpret_cast<const float4 *>(v + (int64_t)col[p] * ld_v + sub * 4);
-        float s = uq.x * vk.x + uq.y * vk.y + uq.z * vk.z + uq.w * vk.w;
-        for (int m = hs >> 1; m >= 1; m >>= 1) s += shfl_xor_f(s, m);
-        if (ok && (sub % hs) == 0) {
-            const int64_t ed = eid ? eid[p] : p;
-            out[ed * h + sub / hs] = s;
+    // U edge groups per trip: their v-row gathers are all issued before the
+    // dots (at h*d = 256 a wave takes one edge at a time, so one gather in
+    // flight per wave would leave the HBM latency exposed)
+    constexpr int U = 4;
+    for (int64_t base = b; base < e; base += U * EPW) {
+        float4 vk[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t p = base + j * EPW + eg;
+            vk[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (p < e) vk[j] = *reinterpret_cast<const float4 *>(v + (int64_t)col[p] * ld_v + sub * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t p = base + j * EPW + eg;
+            float s = uq.x * vk[j].x + uq.y * vk[j].y + uq.z * vk[j].z + uq.w * vk[j].w;
+            for (int m = hs >> 1; m >= 1; m >>= 1) s += shfl_xor_f(s, m);
+            if (p < e && (sub % hs) == 0) {
+                const int64_t ed = eid ? eid[p] : p;
+                out[ed * h + sub / hs] = s;
+            }
         }
     }
 }

@@ -435,6 +435,34 @@ __global__ __launch_bounds__(256) void att_softmax_bwd_g16_kernel(
     }
 }
 
+// gspmm copy_rhs sum / max with 16 lanes per row and all H heads per lane
+// (the segment_reduce_kernel above takes a wave per row and a pass per head).
+template <int H>
+__global__ __launch_bounds__(256) void segment_reduce_g16_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr,
+                                                                 const int64_t *__restrict__ eid,
+                                                                 const float *__restrict__ x, int reduce,
+                                                                 float *__restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int sub = threadIdx.x & 15;
+    const bool live = r < n_rows;
+    const int64_t b = live ? row_ptr[r] : 0, e = live ? row_ptr[r + 1] : 0;
+    float a[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) a[j] = reduce ? -INFINITY : 0.f;
+    for (int64_t p = b + sub; p < e; p += 16) {
+        float v[H];
+        load_heads<H>(x, eid ? eid[p] : p, v);
+#pragma unroll
+        for (int j = 0; j < H; ++j) a[j] = reduce ? fmaxf(a[j], v[j]) : a[j] + v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) a[j] = reduce ? g16_max(a[j]) : g16_sum(a[j]);
+    if (live && sub == 0) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) out[r * H + j] = (b == e) ? 0.f : a[j];
+    }
+}
+
 // ---------------------------------------------------------------- value kernels
 __global__ void edge_dropout_kernel(int64_t n, const float *__restrict__ val,
                                     const float *__restrict__ rand, float keep,
@@ -511,8 +539,19 @@ extern "C" int igr_segment_reduce_f32(const igr_csr *g, int32_t h, const float *
         if (reduce != 0 && reduce != 1) return arg_error(fn, "reduce must be 0 (sum) or 1 (max)");
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-        hipLaunchKernelGGL(segment_reduce_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256),
-                           0, st, g->n_rows, h, g->row_ptr, g->edge_id, x, reduce, out);
+        const dim3 g16((unsigned)((g->n_rows + 15) / 16));
+        const bool vec = (reinterpret_cast<uintptr_t>(x) & 15u) == 0;
+#define IGR_SR(HH) \
+    hipLaunchKernelGGL((segment_reduce_g16_kernel<HH>), g16, dim3(256), 0, st, g->n_rows, g->row_ptr, g->edge_id, x, \
+                       reduce, out)
+        if (h == 1) IGR_SR(1);
+        else if (h == 2) IGR_SR(2);
+        else if (h == 4 && vec) IGR_SR(4);
+        else if (h == 8 && vec) IGR_SR(8);
+        else
+            hipLaunchKernelGGL(segment_reduce_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256),
+                               0, st, g->n_rows, h, g->row_ptr, g->edge_id, x, reduce, out);
+#undef IGR_SR
         return launch_status(fn);
     });
 }

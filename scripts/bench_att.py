@@ -4,6 +4,7 @@ IGCN's feature graph over the synthetic bipartite graph (feature_ratio 1,
 nnz_F = 2E + N, igr.dist_train.FeatureShard at world 1), H = 4 heads of d:
   sddmm      alpha[e, h] = <q[row_e, h, :], k[col_e, h, :]>      (igr_sddmm_dot_f32)
   softmax    per-row max-shifted exp / sum, head mean            (igr_att_softmax_f32)
+  segment    gspmm copy_rhs max over alpha (the DGL-surface op)   (igr_segment_reduce_f32)
   spmm       out = SpMM(E, w) with the per-edge attention values (igr_spmm_f32)
 HIP events per launch.  SDDMM algorithmic bytes per SURVEY §8d:
 nnz (8 + 2*4*H*d) + nnz * 4H (q row and k row per edge, no cache credit; the
@@ -66,6 +67,10 @@ def main():
     comp = g.nnz * (4 + 4 * H * d + 4 * H) + g.n_rows * 4 * H * d
     res['sddmm'] = {'ms': ms, 'edges_per_s': g.nnz / ms * 1e3, 'algorithmic_GBps': alg / ms / 1e6,
                     'frac': alg / ms / 1e6 / 8000.0, 'compulsory_GBps': comp / ms / 1e6}
+    ms = timed(lambda: ops.segment_reduce(g, alpha, 'max'), args.steps, args.warmup)
+    byts = g.nnz * 4 * H + g.n_rows * (8 + 4 * H)
+    res['segment_max'] = {'ms': ms, 'edges_per_s': g.nnz / ms * 1e3, 'algorithmic_GBps': byts / ms / 1e6,
+                          'frac': byts / ms / 1e6 / 8000.0}
     holder = {}
 
     def sm():

@@ -148,12 +148,20 @@ def test_sddmm_and_segment_reduce():
         gamma = d * 2.0 ** -24
         assert np.all(np.abs(out[eid] - ref64) <= gamma * mag + 1e-30)
         assert np.all(np.abs(ref - ref64) <= gamma * mag + 1e-30)  # the oracle itself, same bound
-    x = rng.standard_normal((g.nnz, 3)).astype(np.float32)
     A = oracle_csr(g, v)
     eid = g.host()['edge_id']
-    for red in ['sum', 'max']:
-        y = ops.segment_reduce(g, t(x), red).cpu().numpy()
-        close(y, O.segment_reduce(A, x[eid], red), rtol=2e-5)
+    for h in [1, 2, 3, 4, 8]:  # 16-lane kernels for 1/2/4/8, the per-head kernel for 3
+        x = rng.standard_normal((g.nnz, h)).astype(np.float32)
+        y = ops.segment_reduce(g, t(x), 'max').cpu().numpy()
+        np.testing.assert_array_equal(y, O.segment_reduce(A, x[eid], 'max'))  # max is exact
+        y = ops.segment_reduce(g, t(x), 'sum').cpu().numpy()
+        ref = np.zeros((g.n_rows, h))
+        rows = A.rows()
+        np.add.at(ref, rows, x[eid].astype(np.float64))
+        mag = np.zeros((g.n_rows, h))
+        np.add.at(mag, rows, np.abs(x[eid]).astype(np.float64))
+        # a float sum's error is bounded by n * 2^-24 * sum |x|; rows here hold <= ~60 edges
+        assert np.all(np.abs(y - ref) <= 64 * 2.0 ** -24 * mag + 1e-30)
 
 
 def test_att_softmax_forward_backward():

@@ -458,6 +458,41 @@ def test_topk_matches_sorted_reference(n, m, k):
     np.testing.assert_array_equal(val.cpu().numpy(), np.take_along_axis(s, order, 1))
 
 
+@pytest.mark.parametrize('case', ['narrow', 'bin_overflow', 'unaligned', 'gowalla_row', 'k_equals_n'])
+def test_topk_paths(case):
+    """The two selection paths of igr_topk (candidates of the k-th value's 12-bit bin
+    in LDS; radix passes over the row when that bin overflows the LDS list), float4
+    and scalar row loads, against a stable numpy sort."""
+    rng = np.random.default_rng(7)
+    n, m, k, ld = 16, 5000, 100, None
+    if case == 'narrow':  # every value in [1, 1.01): one 12-bit bin, ~1000 candidates, many ties
+        s = (1 + np.round(rng.random((n, m)) * 0.01, 4)).astype(np.float32)
+    elif case == 'bin_overflow':  # the k-th value's bin holds > 4096 elements
+        m = 20000
+        s = (1 + rng.random((n, m)) * 0.1).astype(np.float32)
+        s[:, ::97] = 5.0
+    elif case == 'unaligned':  # rows not 16-B aligned (odd leading dimension)
+        ld = m + 3
+        s = rng.standard_normal((n, m)).astype(np.float32)
+    elif case == 'gowalla_row':
+        n, m = 40, 40_981
+        s = (rng.standard_normal((n, m)) * 0.05).astype(np.float32)
+        s[:, rng.integers(0, m, 50)] = -np.inf
+    else:
+        m, k = 700, 700
+        s = np.round(rng.standard_normal((n, m)), 1).astype(np.float32)
+    if ld is None:
+        x = t(s)
+    else:
+        buf = torch.zeros(n * ld, dtype=torch.float32, device=DEV)
+        x = buf.view(n, ld)[:, 1:m + 1]  # row starts 4 B past a 16-B boundary
+        x.copy_(t(s))
+    val, idx = ops.topk(x, k)
+    order = np.lexsort((np.broadcast_to(np.arange(m), s.shape), -s.astype(np.float64)), axis=1)[:, :k]
+    np.testing.assert_array_equal(idx.cpu().numpy(), order)
+    np.testing.assert_array_equal(val.cpu().numpy(), np.take_along_axis(s, order, 1))
+
+
 def test_mask_scores_then_topk_matches_torch():
     """mask (absolute row_ptr slice into a bigger CSR) + topk == torch masking + sort."""
     rng = np.random.default_rng(2)

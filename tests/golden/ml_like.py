@@ -17,6 +17,8 @@ SHAPES = {
     # name: (n_users, n_items, mean interactions per user, d, n_layers, epochs)
     'ml100k': (943, 1682, 106, 32, 1, 20),
     'ml1m': (6040, 3706, 165, 64, 2, 10),
+    # the reference's own IGCN depth (config.py:430: n_layers 3, d 64) on the ML-1M shape
+    'ml1m_l3': (6040, 3706, 165, 64, 3, 10),
 }
 
 

@@ -41,11 +41,12 @@ class DS:
         return len(self.train_array)
 
 
-@pytest.mark.parametrize('shape,batch_rep', [('ml100k', 'auto'), ('ml1m', 'auto'), ('ml100k', True)])
+@pytest.mark.parametrize('shape,batch_rep', [('ml100k', 'auto'), ('ml1m', 'auto'), ('ml1m_l3', 'auto'), ('ml100k', True)])
 def test_igcn_training_matches_reference(shape, batch_rep):
     """batch_rep True forces the row-restricted last layer (propagate_rows) on a
     graph where 'auto' would not take it, so that path is pinned to the
-    reference's trajectory too."""
+    reference's trajectory too.  ml1m_l3 is the reference's own IGCN depth
+    (config.py:430, n_layers 3) on the ML-1M shape."""
     path = os.path.join(GOLDEN, f'train_{shape}.npz')
     if not os.path.exists(path):
         pytest.skip(f'{path} not generated')

@@ -6,7 +6,8 @@ sampler (dataset.py:119-131).  BPRBatchSampler draws whole batches with the
 same distribution in vectorised numpy (the reference runs the per-sample
 Python sampler in 6 DataLoader workers, trainer.py:522-526).
 SyntheticDataset builds the benchmark's random bipartite graphs;
-GowallaDataset / MovieLensDataset ingest raw logs.
+GowallaDataset / YelpDataset / AmazonDataset / MovieLensDataset ingest raw logs
+(SURVEY.md §8f row 4).
 """
 import os
 import random
@@ -169,6 +170,50 @@ class GowallaDataset(InteractionDataset):
                          names=['u', 't', 'lat', 'lon', 'i'], dtype={'u': np.int64, 't': str, 'i': np.int64})
         t = pd.to_datetime(df['t'], format='%Y-%m-%dT%H:%M:%SZ', utc=True).astype('int64') // 10 ** 9
         self.load(df['u'].to_numpy(), df['i'].to_numpy(), t.to_numpy())
+
+
+def _first_appearance_codes(ids):
+    """String ids -> int codes numbered in first-appearance order (what the
+    reference's insertion-ordered dicts give), so `ingest` sees the same order."""
+    import pandas as pd
+    return pd.factorize(np.asarray(ids, dtype=object), sort=False)[0].astype(np.int64)
+
+
+class YelpDataset(InteractionDataset):
+    """dataset.py:192-223: yelp_academic_dataset_review.json (one JSON record per
+    line); reviews with stars > 3 are interactions, time = 'date'
+    ('%Y-%m-%d %H:%M:%S', parsed as UTC like GowallaDataset)."""
+
+    def __init__(self, dataset_config):
+        super().__init__(dataset_config)
+        import pandas as pd
+        path = os.path.join(dataset_config['path'], 'yelp_academic_dataset_review.json')
+        us, its, ts = [], [], []
+        for chunk in pd.read_json(path, lines=True, dtype=False, convert_dates=False, keep_default_dates=False,
+                                  chunksize=1 << 20):
+            keep = chunk['stars'].astype(np.float64).to_numpy() > 3.
+            c = chunk[keep]
+            us.append(c['user_id'].astype(str).to_numpy())
+            its.append(c['business_id'].astype(str).to_numpy())
+            ts.append((pd.to_datetime(c['date'], format='%Y-%m-%d %H:%M:%S', utc=True).astype('int64')
+                       // 10 ** 9).to_numpy())
+        cat = lambda xs, dt: np.concatenate(xs) if xs else np.zeros(0, dt)  # noqa: E731
+        self.load(_first_appearance_codes(cat(us, object)), _first_appearance_codes(cat(its, object)),
+                  cat(ts, np.int64))
+
+
+class AmazonDataset(InteractionDataset):
+    """dataset.py:226-255: ratings_Books.csv ('user,item,rating,time', no header);
+    ratings > 3 are interactions (the Amazon-Books config of BASELINE.json)."""
+
+    def __init__(self, dataset_config):
+        super().__init__(dataset_config)
+        import pandas as pd
+        df = pd.read_csv(os.path.join(dataset_config['path'], 'ratings_Books.csv'), header=None,
+                         names=['u', 'i', 'r', 't'], dtype={'u': str, 'i': str, 'r': np.float64, 't': np.int64})
+        df = df[df['r'].to_numpy() > 3.]
+        self.load(_first_appearance_codes(df['u'].to_numpy()), _first_appearance_codes(df['i'].to_numpy()),
+                  df['t'].to_numpy())
 
 
 class MovieLensDataset(InteractionDataset):

@@ -80,3 +80,40 @@ def write_checkins(path, n_users=300, n_items=150, n_lines=9000, seed=21):
         for a, b, c in zip(u, i, t):
             ts = _t.strftime('%Y-%m-%dT%H:%M:%SZ', _t.gmtime(int(c)))
             f.write(f'{a}\t{ts}\t30.2\t-97.7\t{b}\n')
+
+
+def _skewed_ids(rng, n, n_lines, s, prefix, width):
+    w = 1.0 / np.arange(1, n + 1) ** s
+    ids = rng.choice(n, n_lines, p=w / w.sum())
+    perm = rng.choice(10 ** width, n, replace=False)  # sparse string ids in no particular order
+    return [f'{prefix}{perm[x]:0{width}d}' for x in ids]
+
+
+def write_amazon_ratings(path, n_users=150, n_items=90, n_lines=9000, seed=23):
+    """A synthetic ratings_Books.csv ('user,item,rating,time', dataset.py:229-244):
+    string ids, ratings 1-5 (only > 3 kept), repeated pairs, timestamp ties."""
+    rng = np.random.default_rng(seed)
+    u = _skewed_ids(rng, n_users, n_lines, 0.8, 'A', 6)
+    i = _skewed_ids(rng, n_items, n_lines, 1.0, '0', 9)
+    r = rng.integers(1, 6, n_lines)
+    t = 1300000000 + rng.integers(0, 2000, n_lines) * 86400
+    with open(path, 'w') as f:
+        for a, b, c, d in zip(u, i, r, t):
+            f.write(f'{a},{b},{float(c)},{d}\n')
+
+
+def write_yelp_reviews(path, n_users=140, n_items=85, n_lines=8500, seed=29):
+    """A synthetic yelp_academic_dataset_review.json (one record per line,
+    dataset.py:196-219): string ids, stars 1-5 (only > 3 kept), 'date' with ties."""
+    import json
+    rng = np.random.default_rng(seed)
+    u = _skewed_ids(rng, n_users, n_lines, 0.8, 'u', 7)
+    i = _skewed_ids(rng, n_items, n_lines, 1.0, 'b', 7)
+    s = rng.integers(1, 6, n_lines)
+    t = 1420070400 + rng.integers(0, 5000, n_lines) * 3600
+    import time as _t
+    with open(path, 'w') as f:
+        for k, (a, b, c, d) in enumerate(zip(u, i, s, t)):
+            rec = {'review_id': f'r{k}', 'user_id': a, 'business_id': b, 'stars': float(c), 'useful': 0,
+                   'text': 'ok', 'date': _t.strftime('%Y-%m-%d %H:%M:%S', _t.gmtime(int(d)))}
+            f.write(json.dumps(rec) + '\n')

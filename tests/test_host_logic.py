@@ -137,6 +137,30 @@ def test_gowalla_ingestion_matches_reference(tmp_path, tag, min_inter):
     assert p.train_data == ds.train_data and p.n_users == ds.n_users
 
 
+@pytest.mark.parametrize('tag,cls,fname,writer', [
+    ('amazon', 'AmazonDataset', 'ratings_Books.csv', 'write_amazon_ratings'),
+    ('yelp', 'YelpDataset', 'yelp_academic_dataset_review.json', 'write_yelp_reviews')])
+@pytest.mark.parametrize('min_inter', [5, 10])
+def test_amazon_yelp_ingestion_matches_reference(tmp_path, tag, cls, fname, writer, min_inter):
+    """dataset.py:192-255 (string ids, rating > 3 filter, then dataset.py:66-114)
+    run by the reference on the same synthetic files (tests/golden/make_ingest_golden.py)."""
+    import os
+    import sys
+    from conftest import GOLDEN
+    sys.path.insert(0, GOLDEN)
+    import ml_like
+    getattr(ml_like, writer)(os.path.join(tmp_path, fname))
+    ref = np.load(os.path.join(GOLDEN, f'ingest_{tag}.npz'))
+    ds = D.get_dataset({'name': cls, 'path': str(tmp_path), 'device': 'cpu', 'min_inter': min_inter,
+                        'split_ratio': [0.8, 0.1, 0.1]})
+    k = f'k{min_inter}'
+    assert [ds.n_users, ds.n_items] == ref[f'{k}_n'].tolist()
+    for split in ['train', 'val', 'test']:
+        data = getattr(ds, split + '_data')
+        np.testing.assert_array_equal(np.cumsum([0] + [len(x) for x in data]), ref[f'{k}_{split}_ptr'])
+        np.testing.assert_array_equal(np.array(sum(data, []), np.int64), ref[f'{k}_{split}_items'])
+
+
 def test_movielens_formats(tmp_path):
     rows = [(1, 10, 5, 100), (1, 20, 3, 50), (2, 10, 4, 70), (2, 30, 1, 10), (1, 30, 4, 20)] * 1
     with open(tmp_path / 'u.data', 'w') as f:

@@ -13,47 +13,74 @@
 namespace igr {
 
 // ---------------------------------------------------------------- SDDMM
-// One wave per destination row.  A node row holds TOT = h*d floats; LPE =
-// TOT/4 lanes read one with a float4 each, so a wave covers EPW = 64/LPE
-// edges at a time.  The row's u slice stays in registers; each edge gathers
-// one v row (TOT*4 bytes) and reduces its d/4-lane head segments with xor
-// shuffles (wave-converged: every lane runs the same trip count).
-template <int TOT>
+// One wave per (destination row, head block).  A launch pass gathers TOT
+// floats of each source row: all h*d of them, or - head split, when one
+// head's slice of v fits an XCD's L2 but the whole table does not - the d of
+// one head, with the grid ordered head-major (blockIdx / row_blocks = head) so
+// the waves running together share one L2-resident slice.  LPE = TOT/4 lanes
+// read a source row with a float4 each; EPW = 64/LPE lane groups per wave each
+// take U consecutive edges of a 64-edge block whose columns came with one
+// coalesced load (broadcast by ds_bpermute).  All U row gathers are issued
+// before any dot.  Head sums: each lane holds U partial dots; a butterfly
+// reduce-scatter over the head's hs = d/4 lanes (masks U/2 .. 1: every step
+// halves the values a lane holds) leaves lane j with edge j's sum over its U
+// lanes - hs - 1 shuffles for U edges instead of U*log2(hs) - then plain xor
+// steps (masks U .. hs/2) finish heads wider than U lanes.  The U writer lanes
+// of a head store U consecutive outputs.
+#ifndef IGR_SDDMM_U
+#define IGR_SDDMM_U 2
+#endif
+template <int TOT, int HS>
 __global__ __launch_bounds__(256) void sddmm_dot_kernel(
     int64_t n_rows, int h, int d, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const int64_t *__restrict__ eid, const float *__restrict__ u,
-    int64_t ld_u, const float *__restrict__ v, int64_t ld_v, float *__restrict__ out) {
+    int64_t ld_u, const float *__restrict__ v, int64_t ld_v, float *__restrict__ out, int64_t row_blocks) {
     constexpr int LPE = TOT / 4;
     constexpr int EPW = 64 / LPE;
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    constexpr int U = HS < IGR_SDDMM_U ? HS : IGR_SDDMM_U;  // edges per group per trip
+    constexpr int TRIP = U * EPW;                            // edges per trip (divides 64)
+    const int64_t hb = (int64_t)blockIdx.x / row_blocks;     // head block (0 unless head split)
+    const int64_t r = ((int64_t)blockIdx.x - hb * row_blocks) * 4 + (threadIdx.x >> 6);
     if (r >= n_rows) return;
     const int lane = threadIdx.x & 63;
     const int eg = lane / LPE;
     const int sub = lane - eg * LPE;
-    const int hs = d / 4;  // lanes per head (power of two, checked by the host)
-    const float4 uq = *reinterpret_cast<const float4 *>(u + r * ld_u + sub * 4);
+    const int lh = sub % HS;  // lane within its head segment
+    const int64_t f0 = hb * TOT;  // first feature of this pass
+    const int head = (int)(f0 / d) + sub / HS;
+    const float4 uq = *reinterpret_cast<const float4 *>(u + r * ld_u + f0 + sub * 4);
+    const float *vs = v + f0 + sub * 4;
     const int64_t b = row_ptr[r], e = row_ptr[r + 1];
-    // U edge groups per trip: their v-row gathers are all issued before the
-    // dots (at h*d = 256 a wave takes one edge at a time, so one gather in
-    // flight per wave would leave the HBM latency exposed)
-    constexpr int U = 4;
-    for (int64_t base = b; base < e; base += U * EPW) {
-        float4 vk[U];
+    for (int64_t base = b; base < e; base += 64) {
+        const int n = (int)min((int64_t)64, e - base);
+        const int cl = lane < n ? col[base + lane] : 0;
+        for (int t = 0; t < n; t += TRIP) {
+            const int k0 = t + eg * U;  // this group's first edge in the block
+            float4 vk[U];
 #pragma unroll
-        for (int j = 0; j < U; ++j) {
-            const int64_t p = base + j * EPW + eg;
-            vk[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (p < e) vk[j] = *reinterpret_cast<const float4 *>(v + (int64_t)col[p] * ld_v + sub * 4);
-        }
-#pragma unroll
-        for (int j = 0; j < U; ++j) {
-            const int64_t p = base + j * EPW + eg;
-            float s = uq.x * vk[j].x + uq.y * vk[j].y + uq.z * vk[j].z + uq.w * vk[j].w;
-            for (int m = hs >> 1; m >= 1; m >>= 1) s += shfl_xor_f(s, m);
-            if (p < e && (sub % hs) == 0) {
-                const int64_t ed = eid ? eid[p] : p;
-                out[ed * h + sub / hs] = s;
+            for (int j = 0; j < U; ++j) {
+                const int c = shfl_i(cl, (k0 + j) & 63);
+                vk[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (k0 + j < n) vk[j] = *reinterpret_cast<const float4 *>(vs + (int64_t)c * ld_v);
             }
+            float sv[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) sv[j] = uq.x * vk[j].x + uq.y * vk[j].y + uq.z * vk[j].z + uq.w * vk[j].w;
+#pragma unroll
+            for (int m = U / 2, cnt = U; m >= 1; m >>= 1, cnt >>= 1) {
+                const bool hi = (lh & m) != 0;
+#pragma unroll
+                for (int i = 0; i < cnt / 2; ++i) {
+                    const float keep = hi ? sv[i + cnt / 2] : sv[i];
+                    const float send = hi ? sv[i] : sv[i + cnt / 2];
+                    sv[i] = keep + shfl_xor_f(send, m);
+                }
+            }
+            float tot = sv[0];
+#pragma unroll
+            for (int m = U; m < HS; m <<= 1) tot += shfl_xor_f(tot, m);
+            const int k = k0 + (lh & (U - 1));
+            if (lh < U && k < n) out[(eid ? eid[base + k] : base + k) * h + head] = tot;
         }
     }
 }
@@ -499,6 +526,41 @@ static unsigned grid_for(int64_t n, int block) {
 
 static bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 
+struct SddmmArgs {
+    const igr_csr *g;
+    int h, d;
+    const float *u;
+    int64_t ld_u;
+    const float *v;
+    int64_t ld_v;
+    float *out;
+    int64_t row_blocks;
+    unsigned grid;
+    hipStream_t st;
+};
+
+template <int T, int HS>
+static void launch_sddmm(const SddmmArgs &a) {
+    if constexpr (HS <= T / 4)  // a head segment lies inside one edge group
+        hipLaunchKernelGGL((sddmm_dot_kernel<T, HS>), dim3(a.grid), dim3(256), 0, a.st, a.g->n_rows, a.h, a.d,
+                           a.g->row_ptr, a.g->col_idx, a.g->edge_id, a.u, a.ld_u, a.v, a.ld_v, a.out,
+                           a.row_blocks);
+}
+
+// TOT floats per pass; d/4 = lanes per head (a power of two <= TOT/4, checked by the caller)
+template <int T>
+static void launch_sddmm_t(const SddmmArgs &a) {
+    switch (a.d / 4) {
+        case 1: launch_sddmm<T, 1>(a); break;
+        case 2: launch_sddmm<T, 2>(a); break;
+        case 4: launch_sddmm<T, 4>(a); break;
+        case 8: launch_sddmm<T, 8>(a); break;
+        case 16: launch_sddmm<T, 16>(a); break;
+        case 32: launch_sddmm<T, 32>(a); break;
+        default: launch_sddmm<T, 64>(a); break;
+    }
+}
+
 }  // namespace igr
 
 using namespace igr;
@@ -512,21 +574,28 @@ extern "C" int igr_sddmm_dot_f32(const igr_csr *g, int32_t h, int32_t d, const f
         if (ld_u < (int64_t)h * d || ld_v < (int64_t)h * d) return arg_error(fn, "leading dimension < h*d");
         if (g->n_rows == 0 || g->nnz == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-        const unsigned blocks = (unsigned)((g->n_rows + 3) / 4);
-        const int tot = h * d;
+        const int64_t row_blocks = (g->n_rows + 3) / 4;
+        const unsigned blocks = (unsigned)row_blocks;
         const bool vec = (d % 4 == 0) && pow2(d / 4) && ld_u % 4 == 0 && ld_v % 4 == 0 &&
                          aligned16(u) && aligned16(v);
-#define IGR_SDDMM(T)                                                                              \
-    hipLaunchKernelGGL((sddmm_dot_kernel<T>), dim3(blocks), dim3(256), 0, st, g->n_rows, h, d,   \
-                       g->row_ptr, g->col_idx, g->edge_id, u, ld_u, v, ld_v, out)
-        if (vec && tot == 64) IGR_SDDMM(64);
-        else if (vec && tot == 128) IGR_SDDMM(128);
-        else if (vec && tot == 256) IGR_SDDMM(256);
-        else if (vec && tot == 32) IGR_SDDMM(32);
+        // head split: one head's slice of v fits an XCD's 4 MB L2, the whole table does not
+        constexpr double kL2 = 3.0 * (1 << 20);
+        const double slice = (double)g->n_cols * d * 4;
+#ifndef IGR_SDDMM_SPLIT
+#define IGR_SDDMM_SPLIT 1
+#endif
+        const bool split = IGR_SDDMM_SPLIT && vec && h > 1 && slice <= kL2 && slice * h > kL2 &&
+                           (d == 32 || d == 64 || d == 128 || d == 256);
+        const int tot = split ? d : h * d;
+        const unsigned grid = split ? (unsigned)(row_blocks * h) : blocks;
+        const SddmmArgs a{g, h, d, u, ld_u, v, ld_v, out, row_blocks, grid, st};
+        if (vec && tot == 64) launch_sddmm_t<64>(a);
+        else if (vec && tot == 128) launch_sddmm_t<128>(a);
+        else if (vec && tot == 256) launch_sddmm_t<256>(a);
+        else if (vec && tot == 32) launch_sddmm_t<32>(a);
         else
             hipLaunchKernelGGL(sddmm_dot_generic, dim3(blocks), dim3(256), 0, st, g->n_rows, h, d,
                                g->row_ptr, g->col_idx, g->edge_id, u, ld_u, v, ld_v, out);
-#undef IGR_SDDMM
         return launch_status(fn);
     });
 }

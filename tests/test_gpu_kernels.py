@@ -164,6 +164,27 @@ def test_sddmm_and_segment_reduce():
         assert np.all(np.abs(y - ref) <= 64 * 2.0 ** -24 * mag + 1e-30)
 
 
+@pytest.mark.parametrize('h,d,dedup', [(4, 64, False), (4, 64, True), (2, 128, True), (4, 32, False), (1, 64, True)])
+def test_sddmm_head_split_and_long_rows(h, d, dedup):
+    """Rows longer than one 64-edge block, edge-id graphs, and the head-split
+    grid (one head's slice of v fits L2, the whole table does not: 6000 x 4 x 64
+    floats = 6.1 MB, a slice 1.5 MB) against the float64 dot-product bound."""
+    nr, nc = 400, 6000
+    g, v = rand_graph(nr, nc, 60000, seed=31 + h + d, skew=True, dedup=dedup)
+    rng = np.random.default_rng(8)
+    q = rng.standard_normal((nr, h * d)).astype(np.float32)
+    k = rng.standard_normal((nc, h * d)).astype(np.float32)
+    out = ops.sddmm_dot(g, t(q), t(k), h).cpu().numpy()
+    A = oracle_csr(g, v)
+    eid = g.host()['edge_id']
+    pos = np.arange(g.nnz) if eid is None else eid
+    rows = A.rows()
+    qq, kk = q.reshape(nr, h, d)[rows].astype(np.float64), k.reshape(nc, h, d)[A.col].astype(np.float64)
+    ref64, mag = (qq * kk).sum(-1), np.abs(qq * kk).sum(-1)
+    assert np.diff(A.row_ptr).max() > 128
+    assert np.all(np.abs(out[pos] - ref64) <= d * 2.0 ** -24 * mag + 1e-30)
+
+
 def test_att_softmax_forward_backward():
     g, v = rand_graph(200, 180, 4000, seed=23, skew=True)
     rng = np.random.default_rng(8)

@@ -164,6 +164,14 @@ int igr_spmm_scaled_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx
                         const float *col_scale, float keep, uint64_t seed, uint64_t offset, int32_t transposed,
                         float *y, int64_t ldy, const igr_epilogue *epi, float *workspace, void *stream);
 
+/* Per-head SpMM: y[r, j*d:(j+1)*d] = sum_{p in row r} rhs[eid(p)*h + j] * x[col[p], j*d:(j+1)*d]
+ * for every head j < h, rhs [nnz, h] by edge id.  The backward of the h-head
+ * SDDMM (AttIGCN.masked_mm, model.py:4246-4255: d x_q = A_alpha x_k per head,
+ * d x_k on the reverse graph) without a per-head copy of rhs.  One launch
+ * per head; same workspace contract as igr_spmm_f32. */
+int igr_spmm_heads_f32(const igr_csr *g, int32_t h, int32_t d, const float *x, int64_t ldx, const float *rhs,
+                       float *y, int64_t ldy, float *workspace, void *stream);
+
 /* Row-restricted SpMM and its transpose (training step: the loss reads the
  * representation only at the batch rows, model.py:4048-4049 / 4049-4051, so
  * the last layer of get_rep, model.py:4196 / 106, is needed only there and

@@ -282,25 +282,27 @@ __device__ __forceinline__ void load_heads(const float *__restrict__ alpha, int6
     }
 }
 
-__device__ __forceinline__ float g16_max(float v) {
+template <int LPR>
+__device__ __forceinline__ float gmax(float v) {
 #pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    for (int o = LPR / 2; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
 }
 
-__device__ __forceinline__ float g16_sum(float v) {
+template <int LPR>
+__device__ __forceinline__ float gsum(float v) {
 #pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    for (int o = LPR / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 
-template <int H, int R>
+template <int H, int R, int LPR>
 __global__ __launch_bounds__(256) void att_softmax_g16_kernel(
     int64_t n_rows, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
     const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d, float *__restrict__ w,
     float *__restrict__ row_max, float *__restrict__ row_sum) {
-    const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
-    const int sub = threadIdx.x & 15;
+    const int64_t r = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
+    const int sub = threadIdx.x % LPR;
     const bool live = r < n_rows;  // every lane stays for the group shuffles
     const int64_t b = live ? row_ptr[r] : 0, e = live ? row_ptr[r + 1] : 0;
     float a[R][H];
@@ -310,7 +312,7 @@ __global__ __launch_bounds__(256) void att_softmax_g16_kernel(
     for (int j = 0; j < H; ++j) m[j] = -INFINITY;
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-        const int64_t p = b + sub + 16 * t;
+        const int64_t p = b + sub + LPR * t;
         k[t] = false;
         if (p < e) {
             const int64_t ed = eid ? eid[p] : p;
@@ -322,7 +324,7 @@ __global__ __launch_bounds__(256) void att_softmax_g16_kernel(
             }
         }
     }
-    for (int64_t p = b + sub + 16 * R; p < e; p += 16) {  // past the register cache
+    for (int64_t p = b + sub + LPR * R; p < e; p += LPR) {  // past the register cache
         const int64_t ed = eid ? eid[p] : p;
         if (!kept(keep, ed)) continue;
         float x[H];
@@ -332,7 +334,7 @@ __global__ __launch_bounds__(256) void att_softmax_g16_kernel(
     }
 #pragma unroll
     for (int j = 0; j < H; ++j) {
-        m[j] = g16_max(m[j]);
+        m[j] = gmax<LPR>(m[j]);
         sm[j] = 0.f;
     }
 #pragma unroll
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(256) void att_softmax_g16_kernel(
                 sm[j] += a[t][j];
             }
         }
-    for (int64_t p = b + sub + 16 * R; p < e; p += 16) {
+    for (int64_t p = b + sub + LPR * R; p < e; p += LPR) {
         const int64_t ed = eid ? eid[p] : p;
         if (!kept(keep, ed)) continue;
         float x[H];
@@ -353,7 +355,7 @@ __global__ __launch_bounds__(256) void att_softmax_g16_kernel(
         for (int j = 0; j < H; ++j) sm[j] += att_exp(x[j], m[j], sqrt_d);
     }
 #pragma unroll
-    for (int j = 0; j < H; ++j) sm[j] = g16_sum(sm[j]);
+    for (int j = 0; j < H; ++j) sm[j] = gsum<LPR>(sm[j]);
     if (!live || b == e) return;
     if (sub == 0) {
 #pragma unroll
@@ -364,7 +366,7 @@ __global__ __launch_bounds__(256) void att_softmax_g16_kernel(
     }
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-        const int64_t p = b + sub + 16 * t;
+        const int64_t p = b + sub + LPR * t;
         if (p < e) {
             const int64_t ed = eid ? eid[p] : p;
             float acc = 0.f;
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(256) void att_softmax_g16_kernel(
             w[ed] = acc;
         }
     }
-    for (int64_t p = b + sub + 16 * R; p < e; p += 16) {
+    for (int64_t p = b + sub + LPR * R; p < e; p += LPR) {
         const int64_t ed = eid ? eid[p] : p;
         if (!kept(keep, ed)) {
             w[ed] = 0.f;
@@ -391,13 +393,13 @@ __global__ __launch_bounds__(256) void att_softmax_g16_kernel(
     }
 }
 
-template <int H, int R>
+template <int H, int R, int LPR>
 __global__ __launch_bounds__(256) void att_softmax_bwd_g16_kernel(
     int64_t n_rows, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
     const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d, const float *__restrict__ row_max,
     const float *__restrict__ row_sum, const float *__restrict__ dw, float *__restrict__ dalpha) {
-    const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
-    const int sub = threadIdx.x & 15;
+    const int64_t r = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
+    const int sub = threadIdx.x % LPR;
     const bool live = r < n_rows;
     const int64_t b = live ? row_ptr[r] : 0, e = live ? row_ptr[r + 1] : 0;
     float m[H], s[H], S[H];
@@ -412,7 +414,7 @@ __global__ __launch_bounds__(256) void att_softmax_bwd_g16_kernel(
     bool k[R];
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-        const int64_t p = b + sub + 16 * t;
+        const int64_t p = b + sub + LPR * t;
         k[t] = false;
         g[t] = 0.f;
         if (p < e) {
@@ -429,7 +431,7 @@ __global__ __launch_bounds__(256) void att_softmax_bwd_g16_kernel(
             }
         }
     }
-    for (int64_t p = b + sub + 16 * R; p < e; p += 16) {
+    for (int64_t p = b + sub + LPR * R; p < e; p += LPR) {
         const int64_t ed = eid ? eid[p] : p;
         if (!kept(keep, ed)) continue;
         const float gg = dw[ed] * inv_h;
@@ -439,19 +441,19 @@ __global__ __launch_bounds__(256) void att_softmax_bwd_g16_kernel(
         for (int j = 0; j < H; ++j) S[j] += att_exp(x[j], m[j], sqrt_d) / s[j] * gg;
     }
 #pragma unroll
-    for (int j = 0; j < H; ++j) S[j] = g16_sum(S[j]);
+    for (int j = 0; j < H; ++j) S[j] = gsum<LPR>(S[j]);
     if (!live || b == e) return;
     const float c = sqrt_d * 10.f;
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-        const int64_t p = b + sub + 16 * t;
+        const int64_t p = b + sub + LPR * t;
         if (p < e) {
             const int64_t ed = eid ? eid[p] : p;
 #pragma unroll
             for (int j = 0; j < H; ++j) dalpha[ed * H + j] = k[t] ? a[t][j] * (g[t] - S[j]) / c : 0.f;
         }
     }
-    for (int64_t p = b + sub + 16 * R; p < e; p += 16) {
+    for (int64_t p = b + sub + LPR * R; p < e; p += LPR) {
         const int64_t ed = eid ? eid[p] : p;
         const bool kk = kept(keep, ed);
         const float gg = dw[ed] * inv_h;
@@ -464,26 +466,26 @@ __global__ __launch_bounds__(256) void att_softmax_bwd_g16_kernel(
 
 // gspmm copy_rhs sum / max with 16 lanes per row and all H heads per lane
 // (the segment_reduce_kernel above takes a wave per row and a pass per head).
-template <int H>
+template <int H, int LPR>
 __global__ __launch_bounds__(256) void segment_reduce_g16_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr,
                                                                  const int64_t *__restrict__ eid,
                                                                  const float *__restrict__ x, int reduce,
                                                                  float *__restrict__ out) {
-    const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
-    const int sub = threadIdx.x & 15;
+    const int64_t r = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
+    const int sub = threadIdx.x % LPR;
     const bool live = r < n_rows;
     const int64_t b = live ? row_ptr[r] : 0, e = live ? row_ptr[r + 1] : 0;
     float a[H];
 #pragma unroll
     for (int j = 0; j < H; ++j) a[j] = reduce ? -INFINITY : 0.f;
-    for (int64_t p = b + sub; p < e; p += 16) {
+    for (int64_t p = b + sub; p < e; p += LPR) {
         float v[H];
         load_heads<H>(x, eid ? eid[p] : p, v);
 #pragma unroll
         for (int j = 0; j < H; ++j) a[j] = reduce ? fmaxf(a[j], v[j]) : a[j] + v[j];
     }
 #pragma unroll
-    for (int j = 0; j < H; ++j) a[j] = reduce ? g16_max(a[j]) : g16_sum(a[j]);
+    for (int j = 0; j < H; ++j) a[j] = reduce ? gmax<LPR>(a[j]) : gsum<LPR>(a[j]);
     if (live && sub == 0) {
 #pragma unroll
         for (int j = 0; j < H; ++j) out[r * H + j] = (b == e) ? 0.f : a[j];
@@ -525,6 +527,14 @@ static unsigned grid_for(int64_t n, int block) {
 }
 
 static bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
+// Rows long enough on average that 64 lanes per row beat 16 (a 16-lane group
+// walking ~200 edges serially leaves the chip latency-bound: ML-1M's feature
+// graph; the synthetic feature graph's ~37-edge rows stay on 16 lanes).
+#ifndef IGR_WIDE_ROW_DEG
+#define IGR_WIDE_ROW_DEG 96
+#endif
+static bool wide_rows(const igr_csr *g) { return g->nnz >= (int64_t)IGR_WIDE_ROW_DEG * g->n_rows; }
 
 struct SddmmArgs {
     const igr_csr *g;
@@ -608,11 +618,16 @@ extern "C" int igr_segment_reduce_f32(const igr_csr *g, int32_t h, const float *
         if (reduce != 0 && reduce != 1) return arg_error(fn, "reduce must be 0 (sum) or 1 (max)");
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-        const dim3 g16((unsigned)((g->n_rows + 15) / 16));
+        const bool wide = wide_rows(g);
+        const dim3 g16((unsigned)((g->n_rows + 15) / 16)), g64((unsigned)((g->n_rows + 3) / 4));
         const bool vec = (reinterpret_cast<uintptr_t>(x) & 15u) == 0;
-#define IGR_SR(HH) \
-    hipLaunchKernelGGL((segment_reduce_g16_kernel<HH>), g16, dim3(256), 0, st, g->n_rows, g->row_ptr, g->edge_id, x, \
-                       reduce, out)
+#define IGR_SR(HH)                                                                                                \
+    if (wide)                                                                                                     \
+        hipLaunchKernelGGL((segment_reduce_g16_kernel<HH, 64>), g64, dim3(256), 0, st, g->n_rows, g->row_ptr,     \
+                           g->edge_id, x, reduce, out);                                                           \
+    else                                                                                                          \
+        hipLaunchKernelGGL((segment_reduce_g16_kernel<HH, 16>), g16, dim3(256), 0, st, g->n_rows, g->row_ptr,     \
+                           g->edge_id, x, reduce, out)
         if (h == 1) IGR_SR(1);
         else if (h == 2) IGR_SR(2);
         else if (h == 4 && vec) IGR_SR(4);
@@ -632,11 +647,16 @@ extern "C" int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alp
         if (!g || h <= 0 || h > kMaxHeads) return arg_error(fn, "h must be in [1, 8]");
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-        const dim3 g16((unsigned)((g->n_rows + 15) / 16));
+        const bool wide = wide_rows(g);
+        const dim3 g16((unsigned)((g->n_rows + 15) / 16)), g64((unsigned)((g->n_rows + 3) / 4));
         const bool vec = (reinterpret_cast<uintptr_t>(alpha) & 15u) == 0;
-#define IGR_SM(HH, RR)                                                                                       \
-    hipLaunchKernelGGL((att_softmax_g16_kernel<HH, RR>), g16, dim3(256), 0, st, g->n_rows, g->row_ptr, g->edge_id, \
-                       alpha, keep, sqrt_d, w, row_max, row_sum)
+#define IGR_SM(HH, RR)                                                                                            \
+    if (wide)                                                                                                     \
+        hipLaunchKernelGGL((att_softmax_g16_kernel<HH, RR, 64>), g64, dim3(256), 0, st, g->n_rows, g->row_ptr,   \
+                           g->edge_id, alpha, keep, sqrt_d, w, row_max, row_sum);                                 \
+    else                                                                                                          \
+        hipLaunchKernelGGL((att_softmax_g16_kernel<HH, RR, 16>), g16, dim3(256), 0, st, g->n_rows, g->row_ptr,   \
+                           g->edge_id, alpha, keep, sqrt_d, w, row_max, row_sum)
         if (h == 1) IGR_SM(1, IGR_SOFTMAX_R);
         else if (h == 2) IGR_SM(2, IGR_SOFTMAX_R);
         else if (h == 4 && vec) IGR_SM(4, IGR_SOFTMAX_R);
@@ -659,11 +679,16 @@ extern "C" int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float 
         if (!row_max || !row_sum) return arg_error(fn, "row_max / row_sum required");
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-        const dim3 g16((unsigned)((g->n_rows + 15) / 16));
+        const bool wide = wide_rows(g);
+        const dim3 g16((unsigned)((g->n_rows + 15) / 16)), g64((unsigned)((g->n_rows + 3) / 4));
         const bool vec = (reinterpret_cast<uintptr_t>(alpha) & 15u) == 0;
 #define IGR_SMB(HH, RR)                                                                                           \
-    hipLaunchKernelGGL((att_softmax_bwd_g16_kernel<HH, RR>), g16, dim3(256), 0, st, g->n_rows, g->row_ptr,         \
-                       g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha)
+    if (wide)                                                                                                     \
+        hipLaunchKernelGGL((att_softmax_bwd_g16_kernel<HH, RR, 64>), g64, dim3(256), 0, st, g->n_rows,           \
+                           g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha);            \
+    else                                                                                                          \
+        hipLaunchKernelGGL((att_softmax_bwd_g16_kernel<HH, RR, 16>), g16, dim3(256), 0, st, g->n_rows,           \
+                           g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha)
         if (h == 1) IGR_SMB(1, IGR_SOFTMAX_R);
         else if (h == 2) IGR_SMB(2, IGR_SOFTMAX_R);
         else if (h == 4 && vec) IGR_SMB(4, IGR_SOFTMAX_R);

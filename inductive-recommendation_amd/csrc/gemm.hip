@@ -14,8 +14,17 @@ namespace igr {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 64, BN = 64, BK = 16;
+#ifndef IGR_GEMM_BK
+#define IGR_GEMM_BK 16
+#endif
+constexpr int BM = 64, BN = 64, BK = IGR_GEMM_BK;
+constexpr int LPT = BM * BK / 256;  // elements of each operand tile one thread stages
 
+// One 64x64 output tile per workgroup (2x2 waves of 32x32, 2x2 MFMA 16x16x4 each).
+// K moves through double-buffered LDS tiles of BK; the next tile's global loads
+// are issued before the current tile's MFMAs, so their latency hides under the
+// math (one barrier per K step: a buffer is rewritten only after every wave has
+// passed the barrier that follows its last read).
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void gemm_f32_mfma(int64_t M, int64_t N, int64_t K,
                                                      const float *__restrict__ A, int64_t lda,
@@ -29,8 +38,8 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(int64_t M, int64_t N, int64
     const int64_t k_hi = k_lo + kc < K ? k_lo + kc : K;
     C += (int64_t)blockIdx.z * zstride;
     // LDS images [k][m] and [k][n], padded by one float to break bank strides.
-    __shared__ float As[BK][BM + 1];
-    __shared__ float Bs[BK][BN + 1];
+    __shared__ float As[2][BK][BM + 1];
+    __shared__ float Bs[2][BK][BN + 1];
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
     const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves, 32x32 each
@@ -41,41 +50,60 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(int64_t M, int64_t N, int64
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int64_t k0 = k_lo; k0 < k_hi; k0 += BK) {
+    // staging coordinates of element i of this thread (same for every K step)
+    auto a_mk = [&](int i, int &mm, int &kk) {
+        const int idx = t + i * 256;
+        if (TA) { kk = idx / BM; mm = idx % BM; }  // a[k*lda + m]: m contiguous
+        else { mm = idx / BK; kk = idx % BK; }     // a[m*lda + k]: k contiguous
+    };
+    auto b_nk = [&](int i, int &nn, int &kk) {
+        const int idx = t + i * 256;
+        if (TB) { kk = idx / BN; nn = idx % BN; }  // b[k*ldb + n]
+        else { nn = idx / BK; kk = idx % BK; }     // b[n*ldb + k] (Linear weight)
+    };
+    float ra[LPT], rb[LPT];
+    auto load = [&](int64_t k0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int idx = t + i * 256;
-            int mm, kk;
-            if (TA) { kk = idx / BM; mm = idx % BM; }   // a[k*lda + m]: m contiguous
-            else { mm = idx / BK; kk = idx % BK; }      // a[m*lda + k]: k contiguous
-            const int64_t gm = m0 + mm, gk = k0 + kk;
-            float v = 0.f;
-            if (gm < M && gk < k_hi) v = TA ? A[gk * lda + gm] : A[gm * lda + gk];
-            As[kk][mm] = v;
-            int nn;
-            if (TB) { kk = idx / BN; nn = idx % BN; }   // b[k*ldb + n]
-            else { nn = idx / BK; kk = idx % BK; }      // b[n*ldb + k] (Linear weight)
-            const int64_t gn = n0 + nn, gk2 = k0 + kk;
-            float w = 0.f;
-            if (gn < N && gk2 < k_hi) w = TB ? B[gk2 * ldb + gn] : B[gn * ldb + gk2];
-            Bs[kk][nn] = w;
+        for (int i = 0; i < LPT; ++i) {
+            int mm, kk, nn, kb;
+            a_mk(i, mm, kk);
+            b_nk(i, nn, kb);
+            const int64_t gm = m0 + mm, gk = k0 + kk, gn = n0 + nn, gk2 = k0 + kb;
+            ra[i] = (gm < M && gk < k_hi) ? (TA ? A[gk * lda + gm] : A[gm * lda + gk]) : 0.f;
+            rb[i] = (gn < N && gk2 < k_hi) ? (TB ? B[gk2 * ldb + gn] : B[gn * ldb + gk2]) : 0.f;
         }
+    };
+    auto stage = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < LPT; ++i) {
+            int mm, kk, nn, kb;
+            a_mk(i, mm, kk);
+            b_nk(i, nn, kb);
+            As[buf][kk][mm] = ra[i];
+            Bs[buf][kb][nn] = rb[i];
+        }
+    };
+    int buf = 0;
+    if (k_lo < k_hi) load(k_lo);
+    for (int64_t k0 = k_lo; k0 < k_hi; k0 += BK) {
+        stage(buf);
         __syncthreads();
+        if (k0 + BK < k_hi) load(k0 + BK);  // next tile in flight under this tile's MFMAs
 #pragma unroll
         for (int ks = 0; ks < BK; ks += 4) {
             const int kr = ks + (lane >> 4);
             float a[2], b[2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) a[i] = As[kr][wm * 32 + i * 16 + (lane & 15)];
+            for (int i = 0; i < 2; ++i) a[i] = As[buf][kr][wm * 32 + i * 16 + (lane & 15)];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) b[j] = Bs[kr][wn * 32 + j * 16 + (lane & 15)];
+            for (int j = 0; j < 2; ++j) b[j] = Bs[buf][kr][wn * 32 + j * 16 + (lane & 15)];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
         }
-        __syncthreads();
+        buf ^= 1;
     }
     // C/D map of 16x16x4: col = lane & 15, row = (lane >> 4) * 4 + reg
 #pragma unroll
@@ -104,13 +132,19 @@ __global__ void splitk_reduce(int64_t M, int64_t N, int S, const float *__restri
     C[m * ldc + n] = s + (bias ? bias[n] : 0.f);
 }
 
+#ifndef IGR_GEMM_SPLIT_WG
+#define IGR_GEMM_SPLIT_WG 512
+#endif
+#ifndef IGR_GEMM_SPLIT_MINK
+#define IGR_GEMM_SPLIT_MINK 256
+#endif
 // Split count: enough workgroups to fill the chip when the output has few
 // 64x64 tiles and K is long (e.g. a Linear weight gradient, K = node count).
 static int split_count(int64_t m, int64_t n, int64_t k) {
     const int64_t tiles = ((m + BM - 1) / BM) * ((n + BN - 1) / BN);
     if (tiles >= 256 || k < 1024) return 1;
-    int64_t s = (512 + tiles - 1) / tiles;
-    const int64_t smax = k / 256;  // at least 256 of K per split
+    int64_t s = (IGR_GEMM_SPLIT_WG + tiles - 1) / tiles;
+    const int64_t smax = k / IGR_GEMM_SPLIT_MINK;  // at least this much of K per split
     if (s > smax) s = smax;
     if (s > 256) s = 256;
     return s < 1 ? 1 : (int)s;

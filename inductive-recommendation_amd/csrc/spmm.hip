@@ -98,6 +98,14 @@ struct W_ValEid {  // rhs by edge id, edge id = edge_id[p] (multigraph / reverse
     const int64_t *eid;
     __device__ __forceinline__ float operator()(int64_t p, int, int) const { return val[ld_stream(eid + p)]; }
 };
+struct W_ValHead {  // per-head rhs [nnz, h] by edge id (CSR position or edge_id[p]), head j
+    const float *val;
+    const int64_t *eid;
+    int64_t h, j;
+    __device__ __forceinline__ float operator()(int64_t p, int, int) const {
+        return val[(eid ? ld_stream(eid + p) : p) * h + j];
+    }
+};
 // Key of an edge for the dropout draw: its (row, column) in the frame the
 // mask was drawn for (a coalesced graph has one edge per pair), so the reverse
 // graph regenerates the forward's mask from its own (column, row) without
@@ -507,6 +515,25 @@ extern "C" int igr_spmm_scaled_f32(const igr_csr *g, int32_t d, const float *x, 
             return arg_error(fn, "dropout keys need row / column ids below 2^32");
         return run_spmm(fn, g, d, x, ldx, W_Scaled{row_scale, col_scale, keep, seed, offset, transposed ? 1 : 0}, y,
                         ldy, epi, workspace, stream);
+    });
+}
+
+extern "C" int igr_spmm_heads_f32(const igr_csr *g, int32_t h, int32_t d, const float *x, int64_t ldx,
+                                  const float *rhs, float *y, int64_t ldy, float *workspace, void *stream) {
+    return guarded("igr_spmm_heads_f32", [&]() -> int {
+        const char *fn = "igr_spmm_heads_f32";
+        if (!g || h <= 0) return arg_error(fn, "bad graph / h");
+        if (g->nnz > 0 && !rhs) return arg_error(fn, "rhs is NULL");
+        if (ldx < (int64_t)h * d || ldy < (int64_t)h * d) return arg_error(fn, "leading dimension < h*d");
+        // one launch per head: each gathers only its d-column slice of x (the
+        // slices of a small table stay L2-resident)
+        for (int32_t j = 0; j < h; ++j) {
+            const int rc = run_spmm(fn, g, d, x ? x + (int64_t)j * d : nullptr, ldx,
+                                    W_ValHead{rhs, g->edge_id, h, j}, y ? y + (int64_t)j * d : nullptr, ldy,
+                                    nullptr, workspace, stream);
+            if (rc != IGR_OK) return rc;
+        }
+        return IGR_OK;
     });
 }
 

@@ -52,6 +52,7 @@ SIGNATURES = {
     'igr_plan_size': (ctypes.c_int, [c_i64, c_vp, c_i64, c_i64, _P(c_i64), _P(c_i64), _P(c_i64)]),
     'igr_plan_fill': (ctypes.c_int, [c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'igr_spmm_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, _P(IgrEpilogue), c_vp, c_vp]),
+    'igr_spmm_heads_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     'igr_spmm_scaled_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_vp, c_f32, ctypes.c_uint64,
                                            ctypes.c_uint64, c_i32, c_vp, c_i64, _P(IgrEpilogue), c_vp, c_vp]),
     'igr_spmm_rows_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,

@@ -106,6 +106,27 @@ def spmm(g: Graph, x, rhs=None, out=None, epi=None):
     return out
 
 
+def spmm_heads(g: Graph, x, rhs, h, out=None):
+    """Per-head SpMM (igr_spmm_heads_f32): out[:, j*d:(j+1)*d] = A_{rhs[:, j]} x[:, j*d:(j+1)*d],
+    rhs [nnz, h] by edge id - the h-head SDDMM's backward without per-head copies of rhs."""
+    _dev(x, rhs, out)
+    x, ldx = _rows(x)
+    if x.shape[0] < g.n_cols or x.shape[1] % h:
+        raise IgrError(f'spmm_heads: lhs {tuple(x.shape)} for {g.n_cols} source nodes, h={h}')
+    d = x.shape[1] // h
+    rhs = _f32(rhs).contiguous()
+    if rhs.numel() != g.nnz * h:
+        raise IgrError(f'spmm_heads: rhs has {rhs.numel()} values, graph has {g.nnz} edges x {h} heads')
+    if out is None:
+        out = torch.empty(g.n_rows, h * d, dtype=torch.float32, device=x.device)
+    if out.shape[0] < g.n_rows or out.shape[1] != h * d or out.stride(1) != 1 or out.dtype != torch.float32:
+        raise IgrError(f'spmm_heads out {tuple(out.shape)} for {g.n_rows} rows x {h * d}')
+    if g.n_rows:
+        L.call('igr_spmm_heads_f32', ctypes.byref(g.csr), h, d, _p(x), ldx, _p(rhs), _p(out), out.stride(0),
+               _p(g.workspace(d)), _stream())
+    return out
+
+
 class ScaledWeights:
     """Edge weights w = row_scale[r] * col_scale[c], dropout fused in-kernel with
     keep probability `keep` and a counter-based mask keyed by (seed, offset,
@@ -358,16 +379,10 @@ class GSDDMMDot(torch.autograd.Function):
         g, h = ctx.g, ctx.h
         du = dv = None
         dout = dout.contiguous()
-        d = u.shape[1] // h
         if ctx.needs_input_grad[1]:
-            du = torch.empty_like(u)
-            for j in range(h):
-                spmm(g, v[:, j * d:(j + 1) * d], dout[:, j].contiguous(), out=du[:, j * d:(j + 1) * d])
+            du = spmm_heads(g, v, dout, h, out=torch.empty_like(u))
         if ctx.needs_input_grad[2]:
-            dv = torch.empty_like(v)
-            rg = g.reverse()
-            for j in range(h):
-                spmm(rg, u[:, j * d:(j + 1) * d], dout[:, j].contiguous(), out=dv[:, j * d:(j + 1) * d])
+            dv = spmm_heads(g.reverse(), u, dout, h, out=torch.empty_like(v))
         return None, du, dv, None
 
 

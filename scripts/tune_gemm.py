@@ -1,0 +1,75 @@
+"""MFMA GEMM variants (scripts/tune_gemm.py build | run): the AttIGCN / NGCF
+projection shapes at ML-1M and synthetic scale, their weight gradients (split-K)
+and the eval score GEMM (users x d by items x d).  `build` compiles one libigr
+per macro set (CPU side); `run` times each in its own process (IGR_LIB)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, 'inductive-recommendation_amd')
+VARIANTS = {
+    'bk16_wg512_k256': '-DIGR_GEMM_BK=16 -DIGR_GEMM_SPLIT_WG=512 -DIGR_GEMM_SPLIT_MINK=256',
+    'bk32_wg1024_k128': '-DIGR_GEMM_BK=32 -DIGR_GEMM_SPLIT_WG=1024 -DIGR_GEMM_SPLIT_MINK=128',
+    'bk32_wg2048_k64': '-DIGR_GEMM_BK=32 -DIGR_GEMM_SPLIT_WG=2048 -DIGR_GEMM_SPLIT_MINK=64',
+    'bk16_wg1024_k64': '-DIGR_GEMM_BK=16 -DIGR_GEMM_SPLIT_WG=1024 -DIGR_GEMM_SPLIT_MINK=64',
+    'bk64_wg1024_k128': '-DIGR_GEMM_BK=64 -DIGR_GEMM_SPLIT_WG=1024 -DIGR_GEMM_SPLIT_MINK=128',
+}
+# name: (m, n, k, trans_a, trans_b)
+SHAPES = {
+    'att_fwd_ml1m': (9748, 256, 64, False, False), 'att_dx_ml1m': (9748, 64, 256, False, True),
+    'att_dw_ml1m': (256, 64, 9748, True, True),
+    'att_fwd_1m': (1_100_002, 256, 64, False, False), 'att_dw_1m': (256, 64, 1_100_002, True, True),
+    'score_gowalla': (4096, 40981, 128, False, False), 'score_ml1m': (6040, 3706, 64, False, False),
+}
+
+
+def build():
+    sys.path.insert(0, PKG)
+    import build as B
+    base = list(B.CFLAGS)
+    for name, flags in VARIANTS.items():
+        B.CFLAGS = base + flags.split()
+        B.build(lib=os.path.join(PKG, 'variants', f'libigr_{name}.so'), obj=os.path.join(PKG, 'build_v', name))
+        print('built', name, flags)
+
+
+def one(name):
+    if name != 'current':
+        os.environ['IGR_LIB'] = os.path.join(PKG, 'variants', f'libigr_{name}.so')
+    sys.path.insert(0, PKG)
+    import numpy as np
+    import torch
+    from igr import ops
+    dev = torch.device('cuda')
+    res = {'variant': name}
+    for sh, (m, n, k, ta, tb) in SHAPES.items():
+        a = torch.randn(*((k, m) if ta else (m, k)), device=dev)
+        b = torch.randn(*((k, n) if tb else (n, k)), device=dev)
+        for _ in range(3):
+            c = ops.gemm(a, b, trans_a=ta, trans_b=tb)
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+        for e0, e1 in ev:
+            e0.record()
+            ops.gemm(a, b, trans_a=ta, trans_b=tb)
+            e1.record()
+        torch.cuda.synchronize()
+        us = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev])) * 1e3
+        ref = (a.t() if ta else a).double() @ (b if tb else b.t()).double()
+        err = float(((c.double() - ref).abs().max() / ref.abs().max()).item())
+        res[sh] = {'us': us, 'tflops': 2 * m * n * k / us / 1e6, 'max_rel_err': err}
+        del a, b, c, ref
+        torch.cuda.empty_cache()
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == '__main__':
+    if sys.argv[1] == 'build':
+        build()
+    elif sys.argv[1] == 'run':
+        for name in (sys.argv[2:] or ['current'] + list(VARIANTS)):
+            subprocess.run([sys.executable, __file__, 'one', name], check=True, timeout=300)
+    else:
+        one(sys.argv[2])

@@ -185,6 +185,28 @@ def test_sddmm_head_split_and_long_rows(h, d, dedup):
     assert np.all(np.abs(out[pos] - ref64) <= d * 2.0 ** -24 * mag + 1e-30)
 
 
+@pytest.mark.parametrize('h,d,dedup', [(4, 64, False), (4, 64, True), (2, 32, True), (3, 24, False)])
+def test_spmm_heads_matches_per_head_oracle(h, d, dedup):
+    """igr_spmm_heads_f32: head j of the output is the SpMM of x's head-j slice with
+    rhs[:, j] as edge weights (by edge id), on the graph and on its reverse."""
+    nr, nc = 300, 2500
+    g, _ = rand_graph(nr, nc, 40000, seed=5 + h, skew=True, dedup=dedup)
+    rng = np.random.default_rng(9)
+    rhs = rng.standard_normal((g.nnz, h)).astype(np.float32)
+    eid = g.host()['edge_id']
+    for gg, n_src in [(g, nc), (g.reverse(), nr)]:
+        x = rng.standard_normal((n_src, h * d)).astype(np.float32)
+        y = ops.spmm_heads(gg, t(x), t(rhs), h).cpu().numpy()
+        hh = gg.host()
+        e2 = hh['edge_id']
+        for j in range(h):
+            w = np.ascontiguousarray(rhs[:, j] if e2 is None else rhs[e2, j])
+            A = O.CSR(gg.n_rows, gg.n_cols, hh['row_ptr'], hh['col_idx'].astype(np.int64), w)
+            ref = O.spmm64(A, x[:, j * d:(j + 1) * d])
+            close(y[:, j * d:(j + 1) * d], ref)
+    del eid
+
+
 def test_att_softmax_forward_backward():
     g, v = rand_graph(200, 180, 4000, seed=23, skew=True)
     rng = np.random.default_rng(8)

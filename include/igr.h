@@ -159,9 +159,12 @@ int igr_spmm_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx, const
  * pair); transposed = 1 runs g as the reverse of that frame, so the backward
  * regenerates the forward's mask without an edge-id permutation.  Rows and
  * columns < 2^32 when keep < 1.  Same epilogue / workspace contract as
- * igr_spmm_f32. */
+ * igr_spmm_f32.  offset_dev (nullable, device int64): the draw offset is
+ * offset + *offset_dev, read on the device - a step counter kept in HBM, so a
+ * captured hipGraph draws a fresh mask on every replay. */
 int igr_spmm_scaled_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx, const float *row_scale,
-                        const float *col_scale, float keep, uint64_t seed, uint64_t offset, int32_t transposed,
+                        const float *col_scale, float keep, uint64_t seed, uint64_t offset,
+                        const int64_t *offset_dev, int32_t transposed,
                         float *y, int64_t ldy, const igr_epilogue *epi, float *workspace, void *stream);
 
 /* Per-head SpMM: y[r, j*d:(j+1)*d] = sum_{p in row r} rhs[eid(p)*h + j] * x[col[p], j*d:(j+1)*d]
@@ -321,17 +324,25 @@ int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int64_t lda, i
  * user's sorted training list items[row_ptr[u] .. row_ptr[u+1]), neg[b] =
  * uniform item not in that list (rejection, at most max_rounds redraws).
  * Counter-based RNG: the draw is a pure function of (seed, offset, b), so a
- * step is reproducible and needs no RNG state. */
+ * step is reproducible and needs no RNG state.  offset_dev (nullable): offset +
+ * *offset_dev read on the device (hipGraph-captured steps). */
 int igr_bpr_sample(int64_t batch, int64_t n_active, const int32_t *active, const int64_t *row_ptr,
                    const int32_t *items, int64_t n_items, uint64_t seed, uint64_t offset,
-                   int32_t max_rounds, int64_t *users, int64_t *pos, int64_t *neg, void *stream);
+                   const int64_t *offset_dev, int32_t max_rounds, int64_t *users, int64_t *pos, int64_t *neg,
+                   void *stream);
 
 /* Fused Adam step (torch.optim.Adam semantics, amsgrad off; trainer.py:44-46,
  * 555): one pass over p, g, m, v.  `step` is the 1-based
- * step count after increment (bias corrections). */
+ * step count after increment (bias corrections).  step_dev (nullable, device
+ * int64): the step is step + *step_dev and the bias corrections are formed on
+ * the device (hipGraph-captured steps). */
 int igr_adam_f32(int64_t n, float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
                  double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
-                 void *stream);
+                 const int64_t *step_dev, void *stream);
+
+/* *counter += value on the stream (one device int64: the step counter a
+ * captured training step advances at its end). */
+int igr_counter_add(int64_t *counter, int64_t value, void *stream);
 
 #ifdef __cplusplus
 }

@@ -122,14 +122,16 @@ struct W_Scaled {
     const float *rs, *cs;
     float keep;
     uint64_t seed, offset;
+    const int64_t *offset_dev;  // + *offset_dev (a device step counter: hipGraph replays draw fresh masks)
     int swap;
     __device__ __forceinline__ float operator()(int64_t, int c, int r) const {
         float w = rs ? rs[r] : 1.f;
         if (cs) w *= cs[c];
         if (keep < 1.f) {
             const uint64_t k = swap ? edge_key((uint32_t)c, (uint32_t)r) : edge_key((uint32_t)r, (uint32_t)c);
+            const uint64_t off = offset + (offset_dev ? (uint64_t)*offset_dev : 0);
             // random_tensor = keep + U; mask = floor(random_tensor) (model.py:4019-4021)
-            w = (floorf(keep + uniform24(seed, offset, k)) != 0.f) ? w / keep : 0.f;
+            w = (floorf(keep + uniform24(seed, off, k)) != 0.f) ? w / keep : 0.f;
         }
         return w;
     }
@@ -505,7 +507,8 @@ extern "C" int igr_spmm_f32(const igr_csr *g, int32_t d, const float *x, int64_t
 
 extern "C" int igr_spmm_scaled_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx,
                                    const float *row_scale, const float *col_scale, float keep, uint64_t seed,
-                                   uint64_t offset, int32_t transposed, float *y, int64_t ldy,
+                                   uint64_t offset, const int64_t *offset_dev, int32_t transposed, float *y,
+                                   int64_t ldy,
                                    const igr_epilogue *epi, float *workspace, void *stream) {
     return guarded("igr_spmm_scaled_f32", [&]() -> int {
         const char *fn = "igr_spmm_scaled_f32";
@@ -513,7 +516,7 @@ extern "C" int igr_spmm_scaled_f32(const igr_csr *g, int32_t d, const float *x, 
         if (!(keep > 0.f && keep <= 1.f)) return arg_error(fn, "keep must be in (0, 1]");
         if (keep < 1.f && (g->n_rows > 4294967295LL || g->n_cols > 4294967295LL))
             return arg_error(fn, "dropout keys need row / column ids below 2^32");
-        return run_spmm(fn, g, d, x, ldx, W_Scaled{row_scale, col_scale, keep, seed, offset, transposed ? 1 : 0}, y,
+        return run_spmm(fn, g, d, x, ldx, W_Scaled{row_scale, col_scale, keep, seed, offset, offset_dev, transposed ? 1 : 0}, y,
                         ldy, epi, workspace, stream);
     });
 }

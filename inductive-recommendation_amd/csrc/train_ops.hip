@@ -34,9 +34,11 @@ __device__ __forceinline__ bool member(const int32_t *__restrict__ items, int64_
 
 __global__ void bpr_sample_kernel(int64_t batch, int64_t n_active, const int32_t *__restrict__ active,
                                   const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
-                                  int64_t n_items, uint64_t seed, uint64_t offset, int32_t max_rounds,
+                                  int64_t n_items, uint64_t seed, uint64_t offset0,
+                                  const int64_t *__restrict__ offset_dev, int32_t max_rounds,
                                   int64_t *__restrict__ users, int64_t *__restrict__ pos,
                                   int64_t *__restrict__ neg) {
+    const uint64_t offset = offset0 + (offset_dev ? (uint64_t)*offset_dev : 0);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < batch;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int32_t u = active[bounded(draw(seed, offset, i, 0), n_active)];
@@ -58,9 +60,18 @@ __global__ void bpr_sample_kernel(int64_t batch, int64_t n_active, const int32_t
 // p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps); weight_decay adds wd*p to g.
 // omb1 = 1 - beta1 and omb2 = 1 - beta2 are formed in double on the host, as
 // torch forms them from Python floats.
+// step_dev (hipGraph-capturable form): the step is step0 + *step_dev, read on the
+// device, and the bias corrections are formed from it in double here.
 __global__ void adam_kernel(int64_t n, float *__restrict__ p, const float *__restrict__ g,
                             float *__restrict__ m, float *__restrict__ v, float omb1, float b2, float omb2,
-                            float eps, float wd, float step_size, float bc2_sqrt) {
+                            float eps, float wd, float step_size, float bc2_sqrt,
+                            const int64_t *__restrict__ step_dev, int64_t step0, double lr, double beta1,
+                            double beta2) {
+    if (step_dev) {
+        const double t = (double)(step0 + *step_dev);
+        step_size = (float)(lr / (1.0 - pow(beta1, t)));
+        bc2_sqrt = (float)sqrt(1.0 - pow(beta2, t));
+    }
     const int64_t n4 = n >> 2;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -101,35 +112,53 @@ using namespace igr;
 
 extern "C" int igr_bpr_sample(int64_t batch, int64_t n_active, const int32_t *active, const int64_t *row_ptr,
                               const int32_t *items, int64_t n_items, uint64_t seed, uint64_t offset,
-                              int32_t max_rounds, int64_t *users, int64_t *pos, int64_t *neg, void *stream) {
+                              const int64_t *offset_dev, int32_t max_rounds, int64_t *users, int64_t *pos,
+                              int64_t *neg, void *stream) {
     return guarded("igr_bpr_sample", [&]() -> int {
         if (n_active <= 0 || n_items <= 0) return arg_error("igr_bpr_sample", "no active users / items");
         if (max_rounds < 0) return arg_error("igr_bpr_sample", "max_rounds < 0");
         if (batch <= 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         hipLaunchKernelGGL(bpr_sample_kernel, dim3(grid_for(batch, 256)), dim3(256), 0, st, batch, n_active,
-                           active, row_ptr, items, n_items, seed, offset, max_rounds, users, pos, neg);
+                           active, row_ptr, items, n_items, seed, offset, offset_dev, max_rounds, users, pos,
+                           neg);
         return launch_status("igr_bpr_sample");
     });
 }
 
 extern "C" int igr_adam_f32(int64_t n, float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
                             double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
-                            void *stream) {
+                            const int64_t *step_dev, void *stream) {
     return guarded("igr_adam_f32", [&]() -> int {
-        if (step < 1) return arg_error("igr_adam_f32", "step must be >= 1");
+        if (step < (step_dev ? 0 : 1)) return arg_error("igr_adam_f32", "step must be >= 1");
         if (n <= 0) return IGR_OK;
         if (!aligned16(param) || !aligned16(grad) || !aligned16(exp_avg) || !aligned16(exp_avg_sq))
             return arg_error("igr_adam_f32", "buffers must be 16-byte aligned");
         // bias corrections in double on the host, as torch computes them from Python floats
-        const double bc1 = 1.0 - std::pow(beta1, (double)step);
-        const double bc2 = 1.0 - std::pow(beta2, (double)step);
+        const double bc1 = step_dev ? 1.0 : 1.0 - std::pow(beta1, (double)step);
+        const double bc2 = step_dev ? 1.0 : 1.0 - std::pow(beta2, (double)step);
         const float step_size = (float)(lr / bc1);
         const float bc2_sqrt = (float)std::sqrt(bc2);
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         const float omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2);
         hipLaunchKernelGGL(adam_kernel, dim3(grid_for((n + 3) / 4, 256)), dim3(256), 0, st, n, param, grad,
-                           exp_avg, exp_avg_sq, omb1, (float)beta2, omb2, (float)eps, (float)weight_decay, step_size, bc2_sqrt);
+                           exp_avg, exp_avg_sq, omb1, (float)beta2, omb2, (float)eps, (float)weight_decay, step_size, bc2_sqrt,
+                           step_dev, step, lr, beta1, beta2);
         return launch_status("igr_adam_f32");
+    });
+}
+
+namespace igr {
+__global__ void counter_add_kernel(int64_t *ctr, int64_t v) {
+    if (threadIdx.x == 0) *ctr += v;
+}
+}  // namespace igr
+
+extern "C" int igr_counter_add(int64_t *counter, int64_t value, void *stream) {
+    return guarded("igr_counter_add", [&]() -> int {
+        if (!counter) return arg_error("igr_counter_add", "counter is NULL");
+        hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), counter,
+                           value);
+        return launch_status("igr_counter_add");
     });
 }

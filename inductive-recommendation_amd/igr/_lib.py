@@ -54,7 +54,7 @@ SIGNATURES = {
     'igr_spmm_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, _P(IgrEpilogue), c_vp, c_vp]),
     'igr_spmm_heads_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     'igr_spmm_scaled_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_vp, c_f32, ctypes.c_uint64,
-                                           ctypes.c_uint64, c_i32, c_vp, c_i64, _P(IgrEpilogue), c_vp, c_vp]),
+                                           ctypes.c_uint64, c_vp, c_i32, c_vp, c_i64, _P(IgrEpilogue), c_vp, c_vp]),
     'igr_spmm_rows_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                          c_i64, c_f32, c_vp, c_i64, c_vp]),
     'igr_spmm_push_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_f32, c_i32, c_vp,
@@ -82,9 +82,10 @@ SIGNATURES = {
     'igr_gemm_f32': (ctypes.c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp, c_vp,
                                     c_i64, c_vp, c_i64, c_vp]),
     'igr_bpr_sample': (ctypes.c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, ctypes.c_uint64, ctypes.c_uint64,
-                                      c_i32, c_vp, c_vp, c_vp, c_vp]),
+                                      c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     'igr_adam_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,
-                                    ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i64, c_vp]),
+                                    ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i64, c_vp, c_vp]),
+    'igr_counter_add': (ctypes.c_int, [c_vp, c_i64, c_vp]),
 }
 
 _lib = None

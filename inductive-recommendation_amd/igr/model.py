@@ -275,8 +275,10 @@ class IGCN(BasicModel):
         The value is row-constant, so one value per row (feat_base) is kept; the
         per-edge array (feat_vals) is materialised only when asked for."""
         ex = (self.alpha - 1.) / 2. - 0.5
-        self.feat_base = ops.feat_row_values(self.row_sum, ex)
-        self._feat_vals = None
+        # in place once allocated: a captured training step (trainer.StepGraph) holds these pointers
+        self.feat_base = ops.feat_row_values(self.row_sum, ex, out=getattr(self, 'feat_base', None))
+        if getattr(self, '_feat_vals', None) is not None:
+            ops.feat_values(self.feat_mat, self.row_sum, ex, out=self._feat_vals)
 
     @property
     def feat_vals(self):
@@ -338,9 +340,13 @@ class IGCN(BasicModel):
         if self.training and self.dropout > 0 and self.config.get('dropout_rng', 'device') == 'cpu':
             return dropout_values(self, self.feat_vals)
         if self.training and self.dropout > 0:
-            self._drop_step = getattr(self, '_drop_step', -1) + 1
             if not hasattr(self, '_drop_seed'):
                 self._drop_seed = int(self.config.get('seed', torch.initial_seed())) & (2 ** 63 - 1)
+            ctr = getattr(self, 'device_step', None)
+            if ctr is not None:  # hipGraph mode: mask offset = next host step + replays so far (device)
+                return ops.ScaledWeights(self.feat_base, None, 1.0 - self.dropout, self._drop_seed,
+                                         getattr(self, '_drop_step', -1) + 1, offset_dev=ctr)
+            self._drop_step = getattr(self, '_drop_step', -1) + 1
             return ops.ScaledWeights(self.feat_base, None, 1.0 - self.dropout, self._drop_seed, self._drop_step)
         return ops.ScaledWeights(self.feat_base)
 

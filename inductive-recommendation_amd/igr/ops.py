@@ -135,13 +135,15 @@ class ScaledWeights:
     feature graph) this replaces the per-edge value array, the rand tensor and
     the dropout pass.  `swap`: applied to the reverse of that frame."""
 
-    def __init__(self, row_scale=None, col_scale=None, keep=1.0, seed=0, offset=0, swap=False):
+    def __init__(self, row_scale=None, col_scale=None, keep=1.0, seed=0, offset=0, swap=False, offset_dev=None):
         self.row_scale, self.col_scale = row_scale, col_scale
         self.keep, self.seed, self.offset = float(keep), int(seed), int(offset)
         self.swap = bool(swap)
+        self.offset_dev = offset_dev  # device int64 counter added to offset (hipGraph-captured steps)
 
     def transposed(self):
-        return ScaledWeights(self.col_scale, self.row_scale, self.keep, self.seed, self.offset, not self.swap)
+        return ScaledWeights(self.col_scale, self.row_scale, self.keep, self.seed, self.offset, not self.swap,
+                             self.offset_dev)
 
 
 def spmm_scaled(g: Graph, x, w: ScaledWeights, out=None, epi=None):
@@ -158,7 +160,8 @@ def spmm_scaled(g: Graph, x, w: ScaledWeights, out=None, epi=None):
     if out is None:
         out = torch.empty(g.n_rows, d, dtype=torch.float32, device=x.device)
     L.call('igr_spmm_scaled_f32', ctypes.byref(g.csr), d, _p(x), ldx, _p(w.row_scale), _p(w.col_scale), w.keep,
-           ctypes.c_uint64(w.seed & (2 ** 64 - 1)), ctypes.c_uint64(w.offset & (2 ** 64 - 1)), int(w.swap), _p(out),
+           ctypes.c_uint64(w.seed & (2 ** 64 - 1)), ctypes.c_uint64(w.offset & (2 ** 64 - 1)), _p(w.offset_dev),
+           int(w.swap), _p(out),
            out.stride(0), None if epi is None else ctypes.byref(epi), _p(g.workspace(d)), _stream())
     return out
 
@@ -171,10 +174,10 @@ def dropout_uniforms(g: Graph, seed, offset, swap=False):
     return out
 
 
-def feat_row_values(row_sum, exponent):
+def feat_row_values(row_sum, exponent, out=None):
     """Per-row row_sum ** exponent (IGCN.update_feat_mat's value, model.py:4127-4130)."""
-    _dev(row_sum)
-    out = torch.empty_like(row_sum)
+    _dev(row_sum, out)
+    out = torch.empty_like(row_sum) if out is None else out
     L.call('igr_feat_values_f32', row_sum.numel(), None, _p(row_sum), float(exponent), _p(out), _stream())
     return out
 
@@ -200,7 +203,8 @@ def _prescale(fw):
 def _feat_spmm_rev(feat, dx, fw, prescaled):
     """demb = F_w^T dx; `prescaled` means dx already carries fw's row scale."""
     if prescaled:
-        return spmm_scaled(feat.reverse(), dx, ScaledWeights(None, None, fw.keep, fw.seed, fw.offset, not fw.swap))
+        return spmm_scaled(feat.reverse(), dx, ScaledWeights(None, None, fw.keep, fw.seed, fw.offset, not fw.swap,
+                                                             fw.offset_dev))
     return _feat_spmm(feat, dx, fw, reverse=True)
 
 

@@ -17,6 +17,20 @@ class Adam(torch.optim.Optimizer):
         if lr < 0 or eps < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
             raise ValueError('invalid Adam hyper-parameters')
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.device_step = None  # (counter, base): step = state step + 1 + *counter, read on the device
+
+    def set_device_step(self, counter):
+        """hipGraph mode: the kernel adds *counter (device int64, the replays so far)
+        to each tensor's step at the time of this call; the host counts stay put
+        until advance_host_steps().  None returns to host-counted steps."""
+        self.device_step = counter
+
+    def advance_host_steps(self, n):
+        for group in self.param_groups:
+            for p in group['params']:
+                st = self.state.get(p)
+                if st:
+                    st['step'] += n
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -39,11 +53,14 @@ class Adam(torch.optim.Optimizer):
                     st['step'] = 0
                     st['exp_avg'] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                st['step'] += 1
+                ctr = self.device_step
+                if ctr is None:
+                    st['step'] += 1
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                 assert p.is_contiguous() and p.dtype == torch.float32
                 L.call('igr_adam_f32', p.numel(), ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(g.data_ptr()),
                        ctypes.c_void_p(st['exp_avg'].data_ptr()), ctypes.c_void_p(st['exp_avg_sq'].data_ptr()),
                        float(group['lr']), float(b1), float(b2), float(group['eps']), float(group['weight_decay']),
-                       st['step'], stream)
+                       st['step'] if ctr is None else st['step'] + 1,
+                       ctypes.c_void_p(0 if ctr is None else ctr.data_ptr()), stream)
         return loss

@@ -41,14 +41,18 @@ class DeviceBPRSampler:
     def __len__(self):
         return (self.length + self.batch_size - 1) // self.batch_size
 
-    def sample(self, n, offset=None):
+    def sample(self, n, offset=None, offset_dev=None):
+        """One batch drawn at counter offset (default: this sampler's step count);
+        with offset_dev (a device int64) the kernel adds *offset_dev on the device,
+        so a captured hipGraph draws a new batch on every replay."""
         offset = self.step if offset is None else offset
         self.step += 1
         users = torch.empty(n, dtype=torch.int64, device=self.device)
         pos, neg = torch.empty_like(users), torch.empty_like(users)
         L.call('igr_bpr_sample', n, len(self.active), ctypes.c_void_p(self.active.data_ptr()),
                ctypes.c_void_p(self.row_ptr.data_ptr()), ctypes.c_void_p(self.items.data_ptr()), self.n_items,
-               ctypes.c_uint64(self.seed), ctypes.c_uint64(offset), self.max_rounds,
+               ctypes.c_uint64(self.seed), ctypes.c_uint64(offset),
+               ctypes.c_void_p(0 if offset_dev is None else offset_dev.data_ptr()), self.max_rounds,
                ctypes.c_void_p(users.data_ptr()), ctypes.c_void_p(pos.data_ptr()), ctypes.c_void_p(neg.data_ptr()),
                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         return users, pos, neg

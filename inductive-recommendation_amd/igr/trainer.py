@@ -12,9 +12,11 @@ eval mode both are the same function of the weights.
 
 Trainer config extensions (all optional): 'sampler': 'device' (default, HIP
 sampler, igr.sampler) or 'host' (vectorised numpy); 'fused' (default True);
-'seed'.  The epoch loss is accumulated on the device and read once per epoch
+'seed'; 'graph' (default False): train_one_epoch replays one hipGraph-captured
+step (StepGraph) instead of issuing every launch from Python.  The epoch loss is accumulated on the device and read once per epoch
 (the reference syncs with loss.item() every step, trainer.py:556).
 """
+import ctypes
 import os
 import sys
 import time
@@ -25,6 +27,7 @@ import torch.nn.functional as F
 from torch.optim import SGD  # noqa: F401  (resolved by name, trainer.py:44-46)
 from torch.optim import Adam as TorchAdam  # noqa: F401
 
+from . import _lib as L
 from . import ops
 from .dataset import AuxiliaryDataset, BPRBatchSampler
 from .optim import Adam  # noqa: F401  fused HIP Adam, resolved by name 'Adam'
@@ -151,6 +154,17 @@ class BasicTrainer:
             self.model.load(self.save_path)
         return self.best_ndcg
 
+    def _graph_epoch(self):
+        """The epoch through a StepGraph when config['graph'] is set and the device
+        sampler is in use; None = run it eagerly (leaving graph mode first)."""
+        if self.config.get('graph', False) and isinstance(self.sampler, DeviceBPRSampler):
+            return graph_epoch(self)
+        sg = getattr(self, '_step_graph', None)
+        if sg is not None:
+            sg.close()
+            self._step_graph = None
+        return None
+
     def calculate_metrics(self, eval_data, rec_items):
         return calculate_metrics(eval_data, rec_items, self.topks)
 
@@ -208,6 +222,97 @@ class BasicTrainer:
         return results, metrics
 
 
+class StepGraph:
+    """One whole training step - device BPR sampling (main + aux batch), the
+    forward, the backward and the fused Adam - captured once in a hipGraph and
+    replayed (the "graph" trainer option).  On graphs the size of ML-1M a step
+    is ~100 short launches whose host-side cost (autograd, ctypes) exceeds the
+    GPU time; a replay issues them with no host work at all.
+
+    Everything that changes from step to step lives on the device: the step
+    counter `ctr` (replays so far) is added on the device to the sampler's
+    counter offset, the dropout-mask offset and Adam's step; the loss is summed
+    into a device scalar; the feature values are updated in place on anneal.
+    So a replay is the same computation as an eager step at the same counters.
+    The host counters are brought forward in close()."""
+
+    def __init__(self, trainer, batch_size, warmup=2):
+        self.tr, self.B = trainer, int(batch_size)
+        model, dev = trainer.model, trainer.sampler.device
+        self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
+        self.aux = getattr(trainer, 'aux_sampler', None)
+        self.s0 = trainer.sampler.step
+        self.a0 = self.aux.step if self.aux is not None else 0
+        self.d0 = getattr(model, '_drop_step', -1)
+        self.n = 0  # real steps run in graph mode (warm-up + replays + eager tails)
+        trainer.opt.set_device_step(self.ctr)
+        model.device_step = self.ctr
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # allocations and lazy state outside the capture
+            for _ in range(warmup):
+                self.body(self.B)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.body(self.B, count=False)
+
+    def body(self, n, count=True):
+        tr = self.tr
+        u, p, ng = tr.sampler.sample(n, offset=self.s0, offset_dev=self.ctr)
+        if self.aux is not None:
+            au, ap, an = self.aux.sample(n, offset=self.a0, offset_dev=self.ctr)
+            loss = tr.step(u, p, ng, au, ap, an)
+        else:
+            loss = tr.step(u, p, ng)
+        self.loss_sum.add_(loss.detach() * n)
+        L.call('igr_counter_add', ctypes.c_void_p(self.ctr.data_ptr()), 1, ops._stream())
+        if count:
+            self.n += 1
+
+    def replay(self):
+        self.graph.replay()
+        self.n += 1
+
+    def take_loss(self):
+        """Sum of loss * batch over the steps since the last call (one host sync)."""
+        v = float(self.loss_sum)
+        self.loss_sum.zero_()
+        return v
+
+    def close(self):
+        """Back to eager steps: host counters advanced by the steps run here."""
+        tr, model = self.tr, self.tr.model
+        tr.sampler.step = self.s0 + self.n
+        if self.aux is not None:
+            self.aux.step = self.a0 + self.n
+        if hasattr(model, '_drop_seed'):
+            model._drop_step = self.d0 + self.n
+        tr.opt.set_device_step(None)
+        tr.opt.advance_host_steps(self.n)
+        model.device_step = None
+
+
+def graph_epoch(trainer):
+    """train_one_epoch through a StepGraph: ceil(len / B) steps, the last one
+    (a partial batch) run eagerly in the same device-counter mode."""
+    B = trainer.config['batch_size']
+    total = trainer.sampler.length
+    full, tail = divmod(total, B)
+    sg = getattr(trainer, '_step_graph', None)
+    if sg is None:
+        if full < 3:
+            return None
+        sg = trainer._step_graph = StepGraph(trainer, B)
+        full -= 2  # the warm-up steps were real steps of this epoch
+    for _ in range(full):
+        sg.replay()
+    if tail:
+        sg.body(tail)
+    return sg.take_loss() / total
+
+
 def make_sampler(trainer_config, dataset, seed):
     if trainer_config.get('sampler', 'device') == 'device' and torch.device(trainer_config['device']).type == 'cuda':
         return DeviceBPRSampler(dataset, trainer_config['batch_size'], trainer_config['device'], seed or 0)
@@ -244,6 +349,9 @@ class BPRTrainer(BasicTrainer):
         return loss
 
     def train_one_epoch(self):
+        loss = self._graph_epoch()
+        if loss is not None:
+            return loss
         tot, cnt = None, 0
         for batch in self.sampler:
             u, p, n = _dev_batch(batch, self.device)
@@ -287,6 +395,10 @@ class IGCNTrainer(BasicTrainer):
         return loss
 
     def train_one_epoch(self):
+        loss = self._graph_epoch()
+        if loss is not None:
+            self.model.feat_mat_anneal()
+            return loss
         tot, cnt = None, 0
         for main, aux in zip(self.sampler, self.aux_sampler):
             u, p, n = _dev_batch(main, self.device)

@@ -32,6 +32,7 @@ def main():
                     help='last layer only at the batch rows (model.batch_rep_pays)')
     ap.add_argument('--model', default='IGCN', choices=['IGCN', 'AttIGCN', 'LightGCN'])
     ap.add_argument('--eval', action='store_true', help='also time one full eval ranking (Recall@20 path)')
+    ap.add_argument('--graph', action='store_true', help='replay one hipGraph-captured step (trainer.StepGraph)')
     ap.add_argument('--sharded', action='store_true',
                     help='igr.dist_train.ShardedIGCN (one rank per GPU under torch.distributed.run; '
                          'per-rank batch --batch)')
@@ -79,6 +80,12 @@ def main():
             return tr.step(u, p, n)
         au, ap_, an = tr.aux_sampler.sample(args.batch)
         return tr.step(u, p, n, au, ap_, an)
+    if args.graph:
+        sg = T.StepGraph(tr, args.batch)
+
+        def step():  # noqa: F811
+            sg.replay()
+            return sg.loss_sum
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -88,7 +95,11 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     feat_nnz = m.feat_mat.nnz if igcn else 0
-    out = {'model': args.model, 'ms_per_step': el / args.steps * 1e3, 'loss': float(loss), 'n_users': args.n_users,
+    if args.graph:
+        loss = sg.take_loss() / ((args.steps + args.warmup + 2) * args.batch)
+        sg.close()
+    out = {'model': args.model, 'graph': args.graph, 'ms_per_step': el / args.steps * 1e3, 'loss': float(loss),
+           'n_users': args.n_users,
            'n_items': args.n_items, 'n_edges': args.n_edges, 'd': args.d, 'layers': args.layers,
            'adj_nnz': m.norm_adj.nnz, 'feat_nnz': feat_nnz,
            'batch_rep': M.batch_rep_pays(m, args.batch) if args.model == 'IGCN' or not igcn else False,

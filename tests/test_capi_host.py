@@ -186,6 +186,6 @@ def test_new_entry_points_validate_arguments():
     _refused('igr_bpr_fwd_bwd_f32', 4, 2000, F, F, F, 0, 0, F, 2000, F, None, None, 1.0, 0.0, None, None, None, 0,
              F, st, match='1024')
     for keep in (0.0, 1.5):
-        _refused('igr_spmm_scaled_f32', ctypes.byref(rect.csr), 64, F, 64, None, None, keep, 1, 0, 0, F, 64, None,
-                 F, st, match='keep')
+        _refused('igr_spmm_scaled_f32', ctypes.byref(rect.csr), 64, F, 64, None, None, keep, 1, 0, None, 0, F, 64,
+                 None, F, st, match='keep')
     _refused('igr_dropout_uniforms', None, 1, 0, 0, F, st, match='NULL')

@@ -150,19 +150,23 @@ class BasicTrainer:
                     if verbose:
                         print('Early stopping!')
                     break
+        self._close_step_graph()  # load() below rebuilds graph structures a captured step points at
         if self.save_path:
             self.model.load(self.save_path)
         return self.best_ndcg
+
+    def _close_step_graph(self):
+        sg = getattr(self, '_step_graph', None)
+        if sg is not None:
+            sg.close()
+            self._step_graph = None
 
     def _graph_epoch(self):
         """The epoch through a StepGraph when config['graph'] is set and the device
         sampler is in use; None = run it eagerly (leaving graph mode first)."""
         if self.config.get('graph', False) and isinstance(self.sampler, DeviceBPRSampler):
             return graph_epoch(self)
-        sg = getattr(self, '_step_graph', None)
-        if sg is not None:
-            sg.close()
-            self._step_graph = None
+        self._close_step_graph()
         return None
 
     def calculate_metrics(self, eval_data, rec_items):
@@ -246,6 +250,8 @@ class StepGraph:
         self.a0 = self.aux.step if self.aux is not None else 0
         self.d0 = getattr(model, '_drop_step', -1)
         self.n = 0  # real steps run in graph mode (warm-up + replays + eager tails)
+        # the replay reads these objects' device arrays: keep them alive while the graph exists
+        self._keep = [getattr(model, a, None) for a in ('norm_adj', 'norm_vals', 'feat_mat', 'feat_base', 'row_sum')]
         trainer.opt.set_device_step(self.ctr)
         model.device_step = self.ctr
         side = torch.cuda.Stream(device=dev)
@@ -292,6 +298,7 @@ class StepGraph:
         tr.opt.set_device_step(None)
         tr.opt.advance_host_steps(self.n)
         model.device_step = None
+        self.graph = self._keep = None
 
 
 def graph_epoch(trainer):

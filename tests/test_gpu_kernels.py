@@ -611,3 +611,63 @@ def test_att_softmax_heads_keep_edge_ids(h, masked, multigraph):
     # the gradient carries a (g - S) cancellation: bound it on the tensor's scale (h = 1 rows have one element)
     gr, g64 = a.grad.cpu().numpy().astype(np.float64), a64.grad.numpy()
     assert np.all(np.abs(gr - g64) <= 1e-4 * np.abs(g64) + 1e-5 * np.abs(g64).max())
+
+
+def test_empty_graphs_and_odd_widths():
+    """nnz = 0 (every row empty) and n_rows = 0 through SpMM, per-head SpMM,
+    SDDMM, segment reduce and the edge softmax; d not a multiple of 4 takes the
+    generic kernels."""
+    g0, _ = rand_graph(5, 7, 0, seed=1)
+    assert g0.nnz == 0
+    x = t(np.ones((7, 64), np.float32))
+    assert ops.spmm(g0, x).abs().max().item() == 0
+    assert ops.spmm_heads(g0, x, torch.zeros(0, device=DEV), 2).abs().max().item() == 0
+    assert ops.sddmm_dot(g0, t(np.ones((5, 64), np.float32)), x, 2).numel() == 0
+    assert ops.segment_reduce(g0, torch.zeros(0, 2, device=DEV), 'max').abs().max().item() == 0
+    w, _, _ = ops.att_softmax(g0, torch.zeros(0, 4, device=DEV), 8.0)
+    assert w.numel() == 0
+    gn, _ = rand_graph(0, 7, 0, seed=2)
+    assert ops.spmm(gn, x).shape == (0, 64)
+    g, v = rand_graph(60, 40, 900, seed=3)
+    A = oracle_csr(g, v)
+    for d in (3, 30, 66):
+        xd = np.random.default_rng(d).standard_normal((40, d)).astype(np.float32)
+        close(ops.spmm(g, t(xd), t(v)).cpu().numpy(), O.spmm64(A, xd))
+
+
+def test_device_counters_equal_host_counters():
+    """The hipGraph-step forms (a device int64 counter added on the device) give
+    exactly the host-counter results: sampler batches, dropout-SpMM masks and
+    Adam updates (bias corrections formed on the device)."""
+    from igr import sampler as S
+    from igr.optim import Adam
+    rng = np.random.default_rng(4)
+    pairs = np.stack([rng.integers(0, 50, 2000), rng.integers(0, 40, 2000)], 1)
+
+    class DS:
+        n_users, n_items, train_pairs = 50, 40, pairs
+
+        def __len__(self):
+            return len(pairs)
+    smp = S.DeviceBPRSampler(DS(), 256, DEV, seed=9)
+    ctr = torch.tensor([5], dtype=torch.int64, device=DEV)
+    for a, b in zip(smp.sample(256, offset=12), smp.sample(256, offset=7, offset_dev=ctr)):
+        assert torch.equal(a, b)
+    g, _ = rand_graph(300, 200, 5000, seed=6)
+    xs = t(rng.standard_normal((200, 64)).astype(np.float32))
+    rs = t(rng.random(300).astype(np.float32))
+    y1 = ops.spmm_scaled(g, xs, ops.ScaledWeights(rs, None, 0.7, 3, 12))
+    y2 = ops.spmm_scaled(g, xs, ops.ScaledWeights(rs, None, 0.7, 3, 7, offset_dev=ctr))
+    assert torch.equal(y1, y2)
+    p1 = torch.nn.Parameter(t(rng.standard_normal(1000).astype(np.float32)))
+    p2 = torch.nn.Parameter(p1.detach().clone())
+    o1, o2 = Adam([p1], lr=1e-2), Adam([p2], lr=1e-2)
+    steps = torch.zeros(1, dtype=torch.int64, device=DEV)
+    o2.set_device_step(steps)
+    for k in range(4):
+        gr = t(rng.standard_normal(1000).astype(np.float32))
+        p1.grad, p2.grad = gr.clone(), gr.clone()
+        o1.step()
+        o2.step()
+        steps += 1
+    torch.testing.assert_close(p2, p1, rtol=0, atol=0)

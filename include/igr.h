@@ -73,7 +73,9 @@ typedef struct igr_csr {
  * It fuses the layer-mean of LightGCN/IGCN get_rep (model.py:108-109,
  * 4198-4199) and the "+ g/(L+1)" of its backward into the SpMM; row_scale
  * lets the backward pre-scale dx_0 by the feature graph's row scale, so the
- * transposed feature SpMM gathers no per-edge column scale. */
+ * transposed feature SpMM gathers no per-edge column scale.  row_mask /
+ * col_mask restrict a layer to the rows a training step's loss can reach
+ * and its backward to the source rows that carry gradient. */
 typedef struct igr_epilogue {
     float alpha;
     float beta;
@@ -86,6 +88,10 @@ typedef struct igr_epilogue {
     int32_t skip_y;             /* 1: do not store y                             */
     const float *row_scale;     /* [n_rows] or NULL: IGCN's feature row scale    */
                                 /* moved onto the reverse SpMM's source rows     */
+    const uint32_t *row_mask;   /* bitmap [ceil(n_rows/32)] or NULL: rows whose  */
+                                /* bit is clear are skipped (y, acc untouched)   */
+    const uint32_t *col_mask;   /* bitmap [ceil(n_cols/32)] or NULL: edges whose */
+                                /* column bit is clear add nothing, x unread     */
 } igr_epilogue;
 
 /* ------------------------------------------------------------------ misc */
@@ -213,6 +219,10 @@ int igr_spmm_push_f32(const igr_csr *g, int32_t d, const int64_t *rows, int64_t 
  * On the reverse graph, out = A^T G (+ G): igr_spmm_push_f32's result. */
 int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, int32_t *slot,
                     void *stream);
+/* bits |= the selected rows and all their neighbours (square graph): the rows
+ * at which a batch's last layer reads the layer below it (the row_mask of that
+ * layer and the col_mask of its reverse, igr_epilogue). bits: uint32[(n+31)/32]. */
+int igr_rowset_mark_neighbors(const igr_csr *g, int64_t n_sel, const int64_t *rows, uint32_t *bits, void *stream);
 int igr_rowset_sum_f32(int64_t n_sel, int32_t d, const int64_t *rows, const int32_t *slot, const float *src,
                        int64_t lds, float scale, float *agg, int64_t ld_agg, void *stream);
 int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint32_t *bits, const uint32_t *filter,

@@ -41,7 +41,12 @@ struct Epi {
     float acc_div;
     int skip_y;
     const float *row_scale;
+    const uint32_t *row_mask, *col_mask;
 };
+
+__device__ __forceinline__ bool bit_set(const uint32_t *__restrict__ m, int64_t i) {
+    return (m[i >> 5] >> (i & 31)) & 1u;
+}
 
 #ifndef IGR_SPMM_NT_STORE
 #define IGR_SPMM_NT_STORE 0
@@ -149,7 +154,9 @@ struct W_Scaled {
 // group, so divergence between groups is harmless).  Steps of U edges issue
 // all U row gathers before their FMAs; the last partial step masks its
 // out-of-range slots (no load is issued for them).
-template <int U>
+// MASK: a column with cl < 0 (masked out when the pair was loaded) adds
+// nothing and its row is not read.
+template <int U, bool MASK>
 __device__ __forceinline__ float4 gather_block(float4 acc, int cl, float vl, int gbase, int n,
                                                const float *__restrict__ xs, int64_t ldx) {
     int k = 0;
@@ -160,7 +167,12 @@ __device__ __forceinline__ float4 gather_block(float4 acc, int cl, float vl, int
         for (int j = 0; j < U; ++j) {
             const int c = shfl_i(cl, gbase + k + j);
             wv[j] = shfl_f(vl, gbase + k + j);
-            xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
+            if (MASK) {
+                xv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (c >= 0) xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
+            } else {
+                xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
+            }
         }
 #pragma unroll
         for (int j = 0; j < U; ++j) acc = f4_fma(wv[j], xv[j], acc);
@@ -173,7 +185,8 @@ __device__ __forceinline__ float4 gather_block(float4 acc, int cl, float vl, int
             if (k + j < n) {
                 const int c = shfl_i(cl, gbase + k + j);
                 wv[j] = shfl_f(vl, gbase + k + j);
-                xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
+                xv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (!MASK || c >= 0) xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
             }
         }
 #pragma unroll
@@ -187,7 +200,7 @@ __device__ __forceinline__ float4 gather_block(float4 acc, int cl, float vl, int
 // edge j lives in block j / LPR, lane gbase + j % LPR - both compile-time, so
 // all n row gathers are issued before their FMAs (narrow rows, d = 32, where a
 // single LPR-edge block would leave only 8 gathers in flight per group).
-template <int NB, int LPR>
+template <int NB, int LPR, bool MASK>
 __device__ __forceinline__ float4 gather_round(float4 acc, const int (&cl)[NB], const float (&vl)[NB], int gbase,
                                                int n, const float *__restrict__ xs, int64_t ldx) {
     constexpr int BE = NB * LPR;
@@ -198,7 +211,8 @@ __device__ __forceinline__ float4 gather_round(float4 acc, const int (&cl)[NB], 
         if (j < n) {
             const int c = shfl_i(cl[j / LPR], gbase + j % LPR);
             wv[j] = shfl_f(vl[j / LPR], gbase + j % LPR);
-            xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
+            xv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!MASK || c >= 0) xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
         }
     }
 #pragma unroll
@@ -207,7 +221,19 @@ __device__ __forceinline__ float4 gather_round(float4 acc, const int (&cl)[NB], 
     return acc;
 }
 
-template <int D, class W>
+// (col, val) of CSR position p; with a column mask, masked-out columns come back as -1
+template <bool MASK, class W>
+__device__ __forceinline__ void load_pair(const int32_t *__restrict__ col, const W &wfn, int64_t p, int r,
+                                          const uint32_t *__restrict__ cmask, int &c, float &w) {
+    c = ld_stream(col + p);
+    w = wfn(p, c, r);
+    if (MASK && !bit_set(cmask, c)) {
+        c = -1;
+        w = 0.f;
+    }
+}
+
+template <int D, class W, bool MASK>
 __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col, W wfn,
     const float *__restrict__ x, int64_t ldx, const int32_t *__restrict__ order, int64_t n_order,
@@ -227,6 +253,7 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
         const int64_t c = (int64_t)blockIdx.x * 4 + wib;
         if (c >= n_chunks) return;
         const int r = chunk_row[c];
+        if (epi.row_mask && !bit_set(epi.row_mask, r)) return;  // wave-uniform
         const int64_t b = chunk_beg[c];
         const int64_t e = min(b + chunk_edges, row_ptr[r + 1]);
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -234,23 +261,17 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
         int n = (int)min((int64_t)64, e - base);
         int cl = 0;
         float vl = 0.f;
-        if (lane < n) {
-            cl = ld_stream(col + base + lane);
-            vl = wfn(base + lane, cl, r);
-        }
+        if (lane < n) load_pair<MASK>(col, wfn, base + lane, r, epi.col_mask, cl, vl);
         while (n > 0) {
             const int64_t nb = base + 64;
             const int nn = (int)min((int64_t)64, e - nb);
             int cl2 = 0;
             float vl2 = 0.f;
-            if (lane < nn) {
-                cl2 = ld_stream(col + nb + lane);
-                vl2 = wfn(nb + lane, cl2, r);
-            }
+            if (lane < nn) load_pair<MASK>(col, wfn, nb + lane, r, epi.col_mask, cl2, vl2);
             // group grp takes edges [grp*LPR, grp*LPR + LPR) of this 64-edge block,
             // i.e. exactly the (col, val) pairs its own lanes loaded
             const int m = min(max(n - grp * LPR, 0), LPR);
-            acc = gather_block<U>(acc, cl, vl, grp * LPR, m, xs, ldx);
+            acc = gather_block<U, MASK>(acc, cl, vl, grp * LPR, m, xs, ldx);
             base = nb;
             n = nn;
             cl = cl2;
@@ -272,6 +293,8 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
     const int64_t i = w * G + grp;
     if (i >= n_order) return;
     const int r = order[i];
+    // a skipped row's group leaves; shuffles never cross groups, so this is safe
+    if (epi.row_mask && !bit_set(epi.row_mask, r)) return;
     const int64_t b = row_ptr[r], e = row_ptr[r + 1];
     const int gbase = grp * LPR;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -286,10 +309,7 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
         for (int k = 0; k < NB; ++k) {
             cl[k] = 0;
             vl[k] = 0.f;
-            if (k * LPR + sub < n) {
-                cl[k] = ld_stream(col + base + k * LPR + sub);
-                vl[k] = wfn(base + k * LPR + sub, cl[k], r);
-            }
+            if (k * LPR + sub < n) load_pair<MASK>(col, wfn, base + k * LPR + sub, r, epi.col_mask, cl[k], vl[k]);
         }
         while (n > 0) {
             const int64_t nb = base + BE;
@@ -300,12 +320,10 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
             for (int k = 0; k < NB; ++k) {  // next round's pairs, under this round's gathers
                 cl2[k] = 0;
                 vl2[k] = 0.f;
-                if (k * LPR + sub < nn) {
-                    cl2[k] = ld_stream(col + nb + k * LPR + sub);
-                    vl2[k] = wfn(nb + k * LPR + sub, cl2[k], r);
-                }
+                if (k * LPR + sub < nn)
+                    load_pair<MASK>(col, wfn, nb + k * LPR + sub, r, epi.col_mask, cl2[k], vl2[k]);
             }
-            acc = gather_round<NB, LPR>(acc, cl, vl, gbase, n, xs, ldx);
+            acc = gather_round<NB, LPR, MASK>(acc, cl, vl, gbase, n, xs, ldx);
             base = nb;
             n = nn;
 #pragma unroll
@@ -321,20 +339,14 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
     int n = (int)min((int64_t)LPR, e - base);
     int cl = 0;
     float vl = 0.f;
-    if (sub < n) {
-        cl = ld_stream(col + base + sub);
-        vl = wfn(base + sub, cl, r);
-    }
+    if (sub < n) load_pair<MASK>(col, wfn, base + sub, r, epi.col_mask, cl, vl);
     while (n > 0) {
         const int64_t nb = base + LPR;
         const int nn = (int)min((int64_t)LPR, e - nb);
         int cl2 = 0;
         float vl2 = 0.f;
-        if (sub < nn) {
-            cl2 = ld_stream(col + nb + sub);
-            vl2 = wfn(nb + sub, cl2, r);
-        }
-        acc = gather_block<U>(acc, cl, vl, gbase, n, xs, ldx);
+        if (sub < nn) load_pair<MASK>(col, wfn, nb + sub, r, epi.col_mask, cl2, vl2);
+        acc = gather_block<U, MASK>(acc, cl, vl, gbase, n, xs, ldx);
         base = nb;
         n = nn;
         cl = cl2;
@@ -360,6 +372,7 @@ __global__ __launch_bounds__(256) void spmm_combine(const int32_t *__restrict__ 
     const int sub = threadIdx.x - slot * LPR;
     const int64_t i = blockIdx.x;
     if (i >= n_split) return;
+    if (epi.row_mask && !bit_set(epi.row_mask, split_row[i])) return;  // block-uniform
     // 8 independent partial sums per slot keep 8 loads in flight (a hub row's
     // slots each walk ~100+ partials); combined in a fixed tree: deterministic
     constexpr int V = 8;
@@ -395,10 +408,14 @@ __global__ __launch_bounds__(256) void spmm_generic(int64_t n_rows, int d,
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (r >= n_rows) return;
+    if (epi.row_mask && !bit_set(epi.row_mask, r)) return;
     const int64_t b = row_ptr[r], e = row_ptr[r + 1];
     for (int f = lane; f < d; f += 64) {
         float s = 0.f;
-        for (int64_t p = b; p < e; ++p) s = fmaf(wfn(p, col[p], (int)r), x[(int64_t)col[p] * ldx + f], s);
+        for (int64_t p = b; p < e; ++p) {
+            if (epi.col_mask && !bit_set(epi.col_mask, col[p])) continue;
+            s = fmaf(wfn(p, col[p], (int)r), x[(int64_t)col[p] * ldx + f], s);
+        }
         store_row1(epi, r, f, s);
     }
 }
@@ -410,10 +427,16 @@ static void launch_fast(const igr_csr *g, const float *x, int64_t ldx, const W &
     const int64_t chunk_blocks = (g->n_chunks + 3) / 4;
     const int64_t row_blocks = (g->n_order + 4 * G - 1) / (4 * G);
     const int64_t blocks = chunk_blocks + row_blocks;
-    if (blocks > 0)
-        hipLaunchKernelGGL((spmm_main<D, W>), dim3((unsigned)blocks), dim3(256), 0, st, g->row_ptr, g->col_idx,
-                           wfn, x, ldx, g->order, g->n_order, g->chunk_row, g->chunk_beg, g->n_chunks,
-                           g->chunk_edges, ws, chunk_blocks, epi);
+    if (blocks > 0) {
+        if (epi.col_mask)
+            hipLaunchKernelGGL((spmm_main<D, W, true>), dim3((unsigned)blocks), dim3(256), 0, st, g->row_ptr,
+                               g->col_idx, wfn, x, ldx, g->order, g->n_order, g->chunk_row, g->chunk_beg,
+                               g->n_chunks, g->chunk_edges, ws, chunk_blocks, epi);
+        else
+            hipLaunchKernelGGL((spmm_main<D, W, false>), dim3((unsigned)blocks), dim3(256), 0, st, g->row_ptr,
+                               g->col_idx, wfn, x, ldx, g->order, g->n_order, g->chunk_row, g->chunk_beg,
+                               g->n_chunks, g->chunk_edges, ws, chunk_blocks, epi);
+    }
     if (g->n_split > 0)
         hipLaunchKernelGGL((spmm_combine<D>), dim3((unsigned)g->n_split), dim3(256), 0, st, g->split_row,
                            g->split_ptr, g->n_split, ws, epi);
@@ -451,6 +474,8 @@ static int run_spmm(const char *fn, const igr_csr *g, int32_t d, const float *x,
         e.acc_div = epi_in->acc_div;
         e.skip_y = epi_in->skip_y;
         e.row_scale = epi_in->row_scale;
+        e.row_mask = epi_in->row_mask;
+        e.col_mask = epi_in->col_mask;
         if (e.acc_mode < 0 || e.acc_mode > 2) return arg_error(fn, "acc_mode must be 0, 1 or 2");
         if (e.acc_mode && (!e.acc || e.ld_acc < d)) return arg_error(fn, "bad acc");
         if (e.add && e.ld_add < d) return arg_error(fn, "bad ld_add");

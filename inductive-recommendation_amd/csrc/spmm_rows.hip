@@ -180,6 +180,22 @@ __global__ void rowset_mark_kernel(int64_t n, const int64_t *__restrict__ rows, 
     slot[r] = (int32_t)i;  // any one of a repeated row's positions
 }
 
+// bits |= {rows[i]} and every column of those rows (one wave per selected row)
+__global__ __launch_bounds__(256) void rowset_mark_neighbors_kernel(int64_t n, const int64_t *__restrict__ rows,
+                                                                    const int64_t *__restrict__ row_ptr,
+                                                                    const int32_t *__restrict__ col,
+                                                                    uint32_t *__restrict__ bits) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = rows[i];
+    if (lane == 0) atomicOr(bits + (r >> 5), 1u << (r & 31));
+    for (int64_t p = row_ptr[r] + lane; p < row_ptr[r + 1]; p += 64) {
+        const uint32_t c = (uint32_t)col[p];
+        atomicOr(bits + (c >> 5), 1u << (c & 31));
+    }
+}
+
 __global__ void rowset_clear_kernel(int64_t n, const int64_t *__restrict__ rows, uint32_t *__restrict__ bits,
                                     uint32_t *__restrict__ filter) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -301,6 +317,19 @@ extern "C" int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bit
         hipLaunchKernelGGL(rowset_mark_kernel, dim3(blocks_for(n_sel, 256)), dim3(256), 0,
                            reinterpret_cast<hipStream_t>(stream), n_sel, rows, bits, filter, slot);
         return launch_status("igr_rowset_mark");
+    });
+}
+
+extern "C" int igr_rowset_mark_neighbors(const igr_csr *g, int64_t n_sel, const int64_t *rows, uint32_t *bits,
+                                         void *stream) {
+    return guarded("igr_rowset_mark_neighbors", [&]() -> int {
+        if (!g) return arg_error("igr_rowset_mark_neighbors", "graph is NULL");
+        if (n_sel <= 0) return IGR_OK;
+        if (!rows || !bits) return arg_error("igr_rowset_mark_neighbors", "NULL pointer");
+        if (g->n_rows != g->n_cols) return arg_error("igr_rowset_mark_neighbors", "graph must be square");
+        hipLaunchKernelGGL(rowset_mark_neighbors_kernel, dim3(blocks_for(n_sel, 4)), dim3(256), 0,
+                           reinterpret_cast<hipStream_t>(stream), n_sel, rows, g->row_ptr, g->col_idx, bits);
+        return launch_status("igr_rowset_mark_neighbors");
     });
 }
 

@@ -34,7 +34,7 @@ class IgrEpilogue(ctypes.Structure):
     _fields_ = [
         ('alpha', c_f32), ('beta', c_f32), ('add', c_vp), ('ld_add', c_i64),
         ('acc', c_vp), ('ld_acc', c_i64), ('acc_mode', c_i32), ('acc_div', c_f32),
-        ('skip_y', c_i32), ('row_scale', c_vp),
+        ('skip_y', c_i32), ('row_scale', c_vp), ('row_mask', c_vp), ('col_mask', c_vp),
     ]
 
 
@@ -60,6 +60,7 @@ SIGNATURES = {
     'igr_spmm_push_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_f32, c_i32, c_vp,
                                          c_i64, c_vp]),
     'igr_rowset_mark': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'igr_rowset_mark_neighbors': (ctypes.c_int, [_P(IgrCsr), c_i64, c_vp, c_vp, c_vp]),
     'igr_rowset_sum_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_f32, c_vp, c_i64, c_vp]),
     'igr_spmm_pull_marked_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32,
                                                 c_i32, c_vp, c_i64, c_vp]),

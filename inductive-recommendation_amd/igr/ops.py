@@ -57,13 +57,18 @@ def _rows(t):
 
 # ------------------------------------------------------------------ raw ops
 
-def epilogue(alpha=1.0, beta=0.0, add=None, acc=None, acc_mode=0, acc_div=1.0, skip_y=False, row_scale=None):
+def epilogue(alpha=1.0, beta=0.0, add=None, acc=None, acc_mode=0, acc_div=1.0, skip_y=False, row_scale=None,
+             row_mask=None, col_mask=None):
     """struct igr_epilogue for spmm / spmm_scaled.  The struct holds raw device
     pointers, so it also keeps the tensors alive (an inline temporary such as
     `epilogue(add=x * 2)` would otherwise be freed - and its memory reused by
     the caching allocator - before the kernel reads it)."""
     e = L.IgrEpilogue()
-    e._refs = (add, acc, row_scale)
+    e._refs = (add, acc, row_scale, row_mask, col_mask)
+    if row_mask is not None:
+        e.row_mask = row_mask.data_ptr()
+    if col_mask is not None:
+        e.col_mask = col_mask.data_ptr()
     if row_scale is not None:
         _f32(row_scale)
         e.row_scale = row_scale.data_ptr()
@@ -200,12 +205,20 @@ def _prescale(fw):
     return None
 
 
-def _feat_spmm_rev(feat, dx, fw, prescaled):
+def _feat_spmm_rev(feat, dx, fw, prescaled, epi=None):
     """demb = F_w^T dx; `prescaled` means dx already carries fw's row scale."""
     if prescaled:
         return spmm_scaled(feat.reverse(), dx, ScaledWeights(None, None, fw.keep, fw.seed, fw.offset, not fw.swap,
-                                                             fw.offset_dev))
-    return _feat_spmm(feat, dx, fw, reverse=True)
+                                                             fw.offset_dev), epi=epi)
+    return _feat_spmm(feat, dx, fw, reverse=True, epi=epi)
+
+
+def neighbor_mask(adj, rows):
+    """Bitmap of `rows` and all their neighbours in the square graph adj
+    (igr_rowset_mark_neighbors): where a batch's last layer reads the layer below."""
+    mask = torch.zeros((adj.n_rows + 31) // 32, dtype=torch.int32, device=rows.device)
+    L.call('igr_rowset_mark_neighbors', ctypes.byref(adj.csr), rows.numel(), _p(rows), _p(mask), _stream())
+    return mask
 
 
 def sddmm_dot(g: Graph, u, v, h=1, out=None):
@@ -617,7 +630,13 @@ class PropagateRows(torch.autograd.Function):
         demb     = F^T dx_0
     Two full-graph SpMMs fewer per training step than rep = Propagate(...)
     followed by a gather; worth it when the batch rows touch far fewer edges
-    than the graph has (see model.batch_rep_pays)."""
+    than the graph has (see model.batch_rep_pays).
+
+    One level further (symmetric adj): the last layer reads x_{L-1} only at
+    R = rows + their neighbours, so x_{L-1} (x_0 when L = 1) is computed only
+    at R (row_mask), and dx_{L-1} - which is zero off R - is pulled only from
+    R (col_mask) in the first full reverse layer.  Exact: skipped terms are
+    exact zeros."""
 
     @staticmethod
     def forward(ctx, adj, adj_vals, feat, emb, fvals, n_layers, rows, aux=None, w=None):
@@ -635,12 +654,18 @@ class PropagateRows(torch.autograd.Function):
             L.call('igr_bpr_fwd_bwd_f32', au.numel(), emb.shape[1], _p(au), _p(ap), _p(an), 0, int(off), _p(emb),
                    emb.stride(0), _p(w), _p(loss), None, 0.0, 0.0, None, None, None, 0, None, _stream())
             aux_loss = loss.mean()
-        x = _feat_spmm(feat, emb, fvals) if feat is not None else emb.contiguous()
+        mask = neighbor_mask(adj, rows) if (adj.reverse() is adj and adj.n_rows == adj.n_cols) else None
+        ctx.mask = mask
+        em = None if mask is None else epilogue(row_mask=mask)
+        if feat is not None:
+            x = _feat_spmm(feat, emb, fvals, epi=em if n_layers == 1 else None)
+        else:
+            x = emb.contiguous()
         s = None
-        for _ in range(n_layers - 1):
+        for layer in range(n_layers - 1):
             xr = gather_rows(x, rows)
             s = xr if s is None else s.add_(xr)
-            x = spmm(adj, x, adj_vals)
+            x = spmm(adj, x, adj_vals, epi=em if layer == n_layers - 2 else None)
         rep_b = spmm_rows(adj, x, rows, adj_vals, add_g=x, add_i=s, scale=1.0 / L1)
         return rep_b if aux is None else (rep_b, aux_loss)
 
@@ -657,12 +682,17 @@ class PropagateRows(torch.autograd.Function):
         else:
             dx = torch.zeros(adj.n_cols, gs.shape[1], dtype=torch.float32, device=gs.device)
             spmm_push(adj, rows, gs, dx, adj_vals, self_add=True)
+        mask = ctx.mask
         if n_layers > 1:
             at = adj.reverse()
             nxt = torch.empty_like(dx)
             for layer in range(n_layers - 1):
                 last = layer == n_layers - 2
-                spmm(at, dx, adj_vals, out=nxt, epi=epilogue(row_scale=rs) if (last and rs is not None) else None)
+                cm = mask if layer == 0 else None  # dx_{L-1} is zero off the neighbour set
+                epi = None
+                if (last and rs is not None) or cm is not None:
+                    epi = epilogue(row_scale=rs if last else None, col_mask=cm)
+                spmm(at, dx, adj_vals, out=nxt, epi=epi)
                 scatter_add_rows(nxt, rows, gs if not (last and rs is not None) else gs * rs[rows][:, None])
                 dx, nxt = nxt, dx
         elif rs is not None:
@@ -671,7 +701,8 @@ class PropagateRows(torch.autograd.Function):
         if feat is None:
             demb = dx
         else:
-            demb = _feat_spmm_rev(feat, dx, fvals, rs is not None)
+            cm = mask if n_layers == 1 else None
+            demb = _feat_spmm_rev(feat, dx, fvals, rs is not None, epi=None if cm is None else epilogue(col_mask=cm))
             if ctx.emb is not None and ctx.needs_input_grad[4]:
                 dfv = sddmm_dot(feat, dx, ctx.emb, 1).view(-1)
         dw = None

@@ -42,6 +42,12 @@ def spmm_bytes(nnz, n_rows, d):
     return nnz * (4 + 4 + 4 * d) + n_rows * (8 + 4 * d)
 
 
+def compulsory_bytes(nnz, n_rows, n_src, d):
+    """SURVEY.md §8d's informational lower bound: the CSR once, every source row
+    once and every output row once (perfect cache reuse of the gathers)."""
+    return nnz * 8 + n_rows * (8 + 4 * d) + n_src * 4 * d
+
+
 def _cpu_model():
     try:
         with open('/proc/cpuinfo') as f:
@@ -166,6 +172,7 @@ def main():
     stream = torch.cuda.current_stream()
     launches = shard.launches()
     launch_bytes = [spmm_bytes(nnz, n_rows, d) for _, _, _, n_rows, nnz in launches]
+    launch_compulsory = [compulsory_bytes(nnz, n_rows, g_.n_cols, d) for _, g_, _, n_rows, nnz in launches]
     log('launches per step: ' + ', '.join(f'{n}(rows={r}, nnz={z})' for n, _, _, r, z in launches))
 
     def step(events=None):
@@ -236,6 +243,7 @@ def main():
                          'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic,
                          'kernel': f'igr::spmm_main<{d}, igr::W_Val>',
                          'avg_launch_ms': avg_kernel_s * 1e3, 'algorithmic_bytes_per_launch': avg_bytes,
+                         'compulsory_GBps': float(np.mean(launch_compulsory)) / avg_kernel_s / 1e9,
                          'launches': {n: {'ms': float(kern_ms[:, k].mean()), 'rows': int(r), 'nnz': int(z),
                                           'algorithmic_GBps': launch_bytes[k] / float(kern_ms[:, k].mean()) / 1e6}
                                       for k, (n, _g, _s, r, z) in enumerate(launches)}},

@@ -121,6 +121,136 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(int64_t M, int64_t N, int64
         }
 }
 
+// 128x128 output tile per workgroup for the large shapes (the Linear(d, 4d)
+// projection over all nodes, the eval score GEMM): 4 waves of 64x64, each a 4x4
+// grid of 16x16x4 MFMAs, so a K step reads 8 operands from LDS for 16 MFMAs.
+// LDS images are laid out by the operand's global order so that staging stores
+// and operand reads are both bank-conflict free: a k-contiguous operand (A not
+// transposed, B a Linear weight) is kept [m][k] with stride BK+1, an
+// m-contiguous one [k][m] with stride 128+16 (lanes 0-15 and 16-31 of an
+// operand read sit 16 banks apart).  Double-buffered, next tile prefetched.
+constexpr int BT = 128, BKT = 16, LPT2 = BT * BKT / 256;
+constexpr int KSTR = BKT + 1, MSTR = BT + 16;
+
+template <bool TRANS>  // TRANS: [k][x] image (x contiguous in global)
+__device__ __forceinline__ int lds_idx(int x, int k) { return TRANS ? k * MSTR + x : x * KSTR + k; }
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm128_f32_mfma(int64_t M, int64_t N, int64_t K,
+                                                        const float *__restrict__ A, int64_t lda,
+                                                        const float *__restrict__ B, int64_t ldb,
+                                                        const float *__restrict__ bias, float *__restrict__ C,
+                                                        int64_t ldc) {
+    constexpr int IMG = (BT * KSTR > BKT * MSTR) ? BT * KSTR : BKT * MSTR;
+    __shared__ float As[2][IMG];
+    __shared__ float Bs[2][IMG];
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves, 64x64 each
+    const int64_t m0 = (int64_t)blockIdx.x * BT, n0 = (int64_t)blockIdx.y * BT;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // staging coordinates: element i of this thread in a BT x BKT operand tile
+    auto coord = [&](bool trans, int i, int &x, int &k) {
+        const int idx = t + i * 256;
+        if (trans) { k = idx / BT; x = idx % BT; }  // x contiguous in global
+        else { x = idx / BKT; k = idx % BKT; }     // k contiguous in global
+    };
+    float ra[LPT2], rb[LPT2];
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int i = 0; i < LPT2; ++i) {
+            int x, k;
+            coord(TA, i, x, k);
+            const int64_t gm = m0 + x, gk = k0 + k;
+            ra[i] = (gm < M && gk < K) ? (TA ? A[gk * lda + gm] : A[gm * lda + gk]) : 0.f;
+            coord(TB, i, x, k);
+            const int64_t gn = n0 + x, gk2 = k0 + k;
+            rb[i] = (gn < N && gk2 < K) ? (TB ? B[gk2 * ldb + gn] : B[gn * ldb + gk2]) : 0.f;
+        }
+    };
+    auto stage = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < LPT2; ++i) {
+            int x, k;
+            coord(TA, i, x, k);
+            As[buf][lds_idx<TA>(x, k)] = ra[i];
+            coord(TB, i, x, k);
+            Bs[buf][lds_idx<TB>(x, k)] = rb[i];
+        }
+    };
+    int buf = 0;
+    if (K > 0) load(0);
+    for (int64_t k0 = 0; k0 < K; k0 += BKT) {
+        stage(buf);
+        __syncthreads();
+        if (k0 + BKT < K) load(k0 + BKT);
+#pragma unroll
+        for (int ks = 0; ks < BKT; ks += 4) {
+            const int kr = ks + (lane >> 4);
+            float a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = As[buf][lds_idx<TA>(wm * 64 + i * 16 + (lane & 15), kr)];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = Bs[buf][lds_idx<TB>(wn * 64 + j * 16 + (lane & 15), kr)];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        buf ^= 1;
+    }
+    // C through LDS: each wave stages 32 of its 64 rows at a time ([32][64+4]: the
+    // two 16-lane halves of a store sit 16 banks apart), then writes whole 256-B
+    // row segments with 16-B stores instead of 64-B pieces from 16 lanes.
+    constexpr int CS = 68;
+    float *Ws = &As[0][0] + wave * 32 * CS;  // 4 x 8.5 KB within As/Bs (36 KB)
+    static_assert(4 * 32 * CS <= 2 * IMG * 2, "C staging must fit in As + Bs");
+    const bool vec = (ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15u) == 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        __syncthreads();  // every wave is past its last operand read (h = 0) / the previous half's reads
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    Ws[(ii * 16 + (lane >> 4) * 4 + r) * CS + j * 16 + (lane & 15)] = acc[2 * h + ii][j][r];
+        __syncthreads();
+        const int c4 = (lane & 15) * 4;
+        const int64_t gn = n0 + wn * 64 + c4;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (bias) {
+            bv.x = gn < N ? bias[gn] : 0.f;
+            bv.y = gn + 1 < N ? bias[gn + 1] : 0.f;
+            bv.z = gn + 2 < N ? bias[gn + 2] : 0.f;
+            bv.w = gn + 3 < N ? bias[gn + 3] : 0.f;
+        }
+#pragma unroll
+        for (int pass = 0; pass < 8; ++pass) {
+            const int row = pass * 4 + (lane >> 4);
+            const int64_t gm = m0 + wm * 64 + h * 32 + row;
+            if (gm >= M) continue;
+            float4 v = *reinterpret_cast<const float4 *>(Ws + row * CS + c4);
+            v = make_float4(v.x + bv.x, v.y + bv.y, v.z + bv.z, v.w + bv.w);
+            float *cp = C + gm * ldc + gn;
+            if (vec && gn + 3 < N) {
+                *reinterpret_cast<float4 *>(cp) = v;
+            } else {
+                if (gn < N) cp[0] = v.x;
+                if (gn + 1 < N) cp[1] = v.y;
+                if (gn + 2 < N) cp[2] = v.z;
+                if (gn + 3 < N) cp[3] = v.w;
+            }
+        }
+    }
+}
+
 // C[m, n] = bias[n] + sum_z W[z, m, n], z in order (deterministic split-K reduce)
 __global__ void splitk_reduce(int64_t M, int64_t N, int S, const float *__restrict__ W,
                               const float *__restrict__ bias, float *__restrict__ C, int64_t ldc) {
@@ -179,6 +309,23 @@ extern "C" int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int
         float *out = S > 1 ? static_cast<float *>(workspace) : c;
         const int64_t ldo = S > 1 ? n : ldc, zs = S > 1 ? m * n : 0;
         const float *bo = S > 1 ? nullptr : bias;
+#ifndef IGR_GEMM128
+#define IGR_GEMM128 1
+#endif
+        // 128 tiles only when they still give >= 2048 workgroups (8 per CU): on
+        // small shapes the 64 tiles' extra parallelism wins (measured)
+        const int64_t tiles128 = ((m + BT - 1) / BT) * ((n + BT - 1) / BT);
+        if (IGR_GEMM128 && S == 1 && tiles128 >= 2048 && (n + BT - 1) / BT <= 65535) {
+            dim3 g2((unsigned)((m + BT - 1) / BT), (unsigned)((n + BT - 1) / BT));
+#define IGR_GEMM2(TA_, TB_) \
+    hipLaunchKernelGGL((gemm128_f32_mfma<TA_, TB_>), g2, dim3(256), 0, st, m, n, k, a, lda, b, ldb, bias, c, ldc)
+            if (trans_a && trans_b) IGR_GEMM2(true, true);
+            else if (trans_a) IGR_GEMM2(true, false);
+            else if (trans_b) IGR_GEMM2(false, true);
+            else IGR_GEMM2(false, false);
+#undef IGR_GEMM2
+            return launch_status(fn);
+        }
         dim3 grid((unsigned)((m + BM - 1) / BM), (unsigned)((n + BN - 1) / BN), (unsigned)S);
 #define IGR_GEMM(TA_, TB_)                                                                                   \
     hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_>), grid, dim3(256), 0, st, m, n, k, a, lda, b, ldb, bo, out, ldo, \

@@ -10,11 +10,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, 'inductive-recommendation_amd')
 VARIANTS = {
-    'bk16_wg512_k256': '-DIGR_GEMM_BK=16 -DIGR_GEMM_SPLIT_WG=512 -DIGR_GEMM_SPLIT_MINK=256',
-    'bk32_wg1024_k128': '-DIGR_GEMM_BK=32 -DIGR_GEMM_SPLIT_WG=1024 -DIGR_GEMM_SPLIT_MINK=128',
-    'bk32_wg2048_k64': '-DIGR_GEMM_BK=32 -DIGR_GEMM_SPLIT_WG=2048 -DIGR_GEMM_SPLIT_MINK=64',
-    'bk16_wg1024_k64': '-DIGR_GEMM_BK=16 -DIGR_GEMM_SPLIT_WG=1024 -DIGR_GEMM_SPLIT_MINK=64',
-    'bk64_wg1024_k128': '-DIGR_GEMM_BK=64 -DIGR_GEMM_SPLIT_WG=1024 -DIGR_GEMM_SPLIT_MINK=128',
+    'g64': '-DIGR_GEMM128=0',
 }
 # name: (m, n, k, trans_a, trans_b)
 SHAPES = {

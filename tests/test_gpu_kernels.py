@@ -671,3 +671,23 @@ def test_device_counters_equal_host_counters():
         o2.step()
         steps += 1
     torch.testing.assert_close(p2, p1, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize('m,n,k', [(4133, 8197, 33), (16500, 258, 70), (1000, 256, 64)])
+def test_gemm_128_tiles_every_transposition(m, n, k):
+    """The 128x128-tile kernel (no split and >= 2048 such tiles: the first two
+    shapes; the third takes the 64-tile kernel): ragged m / n / k edges, every
+    transposition, bias, against float64."""
+    from igr import _lib
+    assert _lib.lib().igr_gemm_workspace_size(m, n, k) == 0  # no split-K: the 128 path
+    rng = np.random.default_rng(m + n + k)
+    A = rng.standard_normal((m, k)).astype(np.float32)
+    B = rng.standard_normal((k, n)).astype(np.float32)
+    bias = rng.standard_normal(n).astype(np.float32)
+    ref = A.astype(np.float64) @ B.astype(np.float64) + bias
+    for ta in (False, True):
+        for tb in (False, True):
+            a = A.T.copy() if ta else A
+            b = B if tb else B.T.copy()
+            c = ops.gemm(t(a), t(b), t(bias), trans_a=ta, trans_b=tb).cpu().numpy()
+            close(c, ref, rtol=1e-5, atol_row=1e-5)

@@ -241,7 +241,7 @@ def main():
                        'item_source_tiles': shard.item_tiles, 'launches_per_step': nl},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic,
-                         'kernel': f'igr::spmm_main<{d}, igr::W_Val>',
+                         'kernel': f'igr::spmm_main<{d}, igr::W_Val, false>',
                          'avg_launch_ms': avg_kernel_s * 1e3, 'algorithmic_bytes_per_launch': avg_bytes,
                          'compulsory_GBps': float(np.mean(launch_compulsory)) / avg_kernel_s / 1e9,
                          'launches': {n: {'ms': float(kern_ms[:, k].mean()), 'rows': int(r), 'nnz': int(z),

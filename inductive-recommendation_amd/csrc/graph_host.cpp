@@ -85,25 +85,34 @@ extern "C" int igr_csr_from_coo(int64_t n_rows, int64_t n_cols, int64_t nnz, con
         });
         std::vector<int64_t> off(n_rows + 1);
         prefix(cnt.data(), n_rows, off.data());
-        // 3. scatter input positions into row buckets (order inside a bucket is arbitrary)
-        std::vector<int64_t> pos(nnz);
+        // 3. scatter into row buckets (order inside a bucket is arbitrary) a key
+        //    that sorts as (col, input position): (col << 32 | position) when both
+        //    fit, so step 4 sorts plain integers in place (no indirect col[] lookups
+        //    per comparison); the position alone otherwise
+        const bool packed = nnz <= (int64_t)UINT32_MAX;
+        std::vector<uint64_t> key(nnz);
         std::vector<int64_t> cur(off.begin(), off.end() - 1);
         parallel_for(nnz, nt, [&](int64_t b, int64_t e) {
             for (int64_t i = b; i < e; ++i)
-                pos[__atomic_fetch_add(&cur[row[i]], 1, __ATOMIC_RELAXED)] = i;
+                key[__atomic_fetch_add(&cur[row[i]], 1, __ATOMIC_RELAXED)] =
+                    packed ? ((uint64_t)col[i] << 32) | (uint64_t)i : (uint64_t)i;
         });
+        auto pos_of = [&](uint64_t k) -> int64_t { return packed ? (int64_t)(k & 0xffffffffu) : (int64_t)k; };
         // 4. sort each bucket by (col, input position) == stable sort by (row, col);
         //    count the entries each row keeps
         std::vector<int64_t> kept(n_rows, 0);
         parallel_for(n_rows, nt, [&](int64_t b, int64_t e) {
             for (int64_t r = b; r < e; ++r) {
-                int64_t *p0 = pos.data() + off[r], *p1 = pos.data() + off[r + 1];
-                std::sort(p0, p1, [&](int64_t x, int64_t y) {
-                    return col[x] < col[y] || (col[x] == col[y] && x < y);
-                });
+                uint64_t *p0 = key.data() + off[r], *p1 = key.data() + off[r + 1];
+                if (packed)
+                    std::sort(p0, p1);
+                else
+                    std::sort(p0, p1, [&](uint64_t x, uint64_t y) {
+                        return col[x] < col[y] || (col[x] == col[y] && x < y);
+                    });
                 int64_t k = 0;
-                for (int64_t *q = p0; q < p1; ++q)
-                    if (!dedup || q == p0 || col[*q] != col[*(q - 1)]) ++k;
+                for (uint64_t *q = p0; q < p1; ++q)
+                    if (!dedup || q == p0 || col[pos_of(*q)] != col[pos_of(*(q - 1))]) ++k;
                 kept[r] = k;
             }
         });
@@ -113,9 +122,9 @@ extern "C" int igr_csr_from_coo(int64_t n_rows, int64_t n_cols, int64_t nnz, con
             for (int64_t r = b; r < e; ++r) {
                 int64_t o = row_ptr[r] - 1;
                 for (int64_t q = off[r]; q < off[r + 1]; ++q) {
-                    const int64_t i = pos[q];
+                    const int64_t i = pos_of(key[q]);
                     const float v = val ? val[i] : 1.f;
-                    if (dedup && q > off[r] && col[i] == col[pos[q - 1]]) {
+                    if (dedup && q > off[r] && col[i] == col[pos_of(key[q - 1])]) {
                         if (val_out) val_out[o] += v;
                     } else {
                         ++o;

@@ -175,29 +175,36 @@ def main():
     launch_compulsory = [compulsory_bytes(nnz, n_rows, g_.n_cols, d) for _, g_, _, n_rows, nnz in launches]
     log('launches per step: ' + ', '.join(f'{n}(rows={r}, nnz={z})' for n, _, _, r, z in launches))
 
-    def step(events=None):
+    def step(events=None, done=None):
         hook = None
         if events is not None:
             def hook(i, ph):
                 events[i][0 if ph == 'start' else 1].record(stream)
         shard.layer(x_users, x_items, y_users, y_items, hook=hook)
+        if done is not None:
+            done.record(stream)  # after the layer's waits on its all-reduces
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     nl = len(launches)
     ev = [[[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(nl)] for _ in range(args.steps)]
+    ev_done = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for s in range(args.steps):
-        step(ev[s])
+        step(ev[s], ev_done[s])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     kern_ms = np.array([[ev[s][k][0].elapsed_time(ev[s][k][1]) for k in range(nl)] for s in range(args.steps)])
+    # exchange left exposed after the last SpMM of a step (0 at N = 1): the time from the
+    # user-side SpMM's end to the point the stream has waited for every item all-reduce
+    exposed_ms = float(np.mean([ev[s][nl - 1][1].elapsed_time(ev_done[s]) for s in range(args.steps)]))
+    compute_ms = float(kern_ms.sum(1).mean())
 
     stats = torch.tensor([elapsed, float(shard.local_nnz)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -206,6 +213,9 @@ def main():
         n = stats[1:].clone()
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
         elapsed, total_nnz = float(t.item()), int(n.item())
+        ex = torch.tensor([exposed_ms, compute_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(ex, op=dist.ReduceOp.MAX)
+        exposed_ms, compute_ms = float(ex[0]), float(ex[1])
     else:
         total_nnz = shard.local_nnz
     value = total_nnz * args.steps / elapsed
@@ -248,6 +258,9 @@ def main():
                                           'algorithmic_GBps': launch_bytes[k] / float(kern_ms[:, k].mean()) / 1e6}
                                       for k, (n, _g, _s, r, z) in enumerate(launches)}},
             'cpu_baseline': cpu,
+            'per_rank': {'spmm_ms_per_step_max': compute_ms, 'exposed_exchange_ms_per_step_max': exposed_ms,
+                         'note': 'HIP events on the compute stream; the exposed exchange is the wait for the item '
+                                 'all-reduces after the last SpMM of the step (0 at N = 1)'},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -139,7 +139,11 @@ def main():
     dev = torch.device('cuda', dev_index)
     if world > 1:
         if args.dist_backend == 'nccl':
-            dist.init_process_group('nccl', device_id=dev)  # RCCL over xGMI
+            # RCCL over xGMI, its kernels on a high-priority stream so the item
+            # all-reduces progress while the SpMM grid fills the chip
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group('nccl', device_id=dev, pg_options=opts)
         else:
             dist.init_process_group(args.dist_backend)
 

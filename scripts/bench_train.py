@@ -45,7 +45,10 @@ def main():
     if args.sharded and world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', '0')))
-        dist.init_process_group('nccl')
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True  # RCCL on a high-priority stream, as bench.py
+        dist.init_process_group('nccl', device_id=torch.device('cuda', int(os.environ.get('LOCAL_RANK', '0'))),
+                                pg_options=opts)
     dev = torch.device('cuda')
     pairs = synthetic_pairs(args.n_users, args.n_items, args.n_edges, 0)
 

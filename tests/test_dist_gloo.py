@@ -1,4 +1,4 @@
-"""Sharded bipartite propagation (igr/dist.py) on CPU with gloo, world size 2.
+"""Sharded bipartite propagation (igr/dist.py) on CPU with gloo, world sizes 2, 4 and 8.
 
 The partition and the all-reduce exchange are the code under test; the
 rank-local SpMM is the oracle (these CPU tests have no HIP device), and the
@@ -75,7 +75,7 @@ def test_balanced_ranges():
     assert max(loads) - min(loads) <= deg.max()
 
 
-@pytest.mark.parametrize('world,tiles,chunks', [(2, 1, 'auto'), (2, 3, 2)])
+@pytest.mark.parametrize('world,tiles,chunks', [(2, 1, 'auto'), (2, 3, 2), (4, 1, 'auto'), (8, 2, 4)])
 def test_sharded_layer_matches_unsharded(world, tiles, chunks):
     U, I, E, d = 400, 150, 5000, 16
     rng = np.random.default_rng(0)

@@ -50,6 +50,14 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', int(os.environ.get('LOCAL_RANK', '0'))),
                                 pg_options=opts)
     dev = torch.device('cuda')
+    import threading
+    building = threading.Event()
+
+    def heartbeat():  # host-side setup of a 200M-edge graph takes minutes: keep the log moving
+        t_hb = time.time()
+        while not building.wait(30):
+            print(f'... setting up ({time.time() - t_hb:.0f}s)', file=sys.stderr, flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     pairs = synthetic_pairs(args.n_users, args.n_items, args.n_edges, 0)
 
     class DS:
@@ -73,8 +81,9 @@ def main():
     tr = T.get_trainer({'name': 'IGCNTrainer' if igcn else 'BPRTrainer', 'optimizer': 'Adam', 'lr': 1e-3,
                         'l2_reg': 0., 'aux_reg': 0.01, 'device': dev, 'n_epochs': 1, 'batch_size': args.batch,
                         'test_batch_size': 512, 'topks': [20]}, ds, m)
+    building.set()
     print(f'built in {time.time() - t0:.1f}s: adj nnz {m.norm_adj.nnz}' +
-          (f', feat nnz {m.feat_mat.nnz}' if igcn else ''), file=sys.stderr)
+          (f', feat nnz {m.feat_mat.nnz}' if igcn else ''), file=sys.stderr, flush=True)
     m.train()
 
     def step():
@@ -101,7 +110,7 @@ def main():
     if args.graph:
         loss = sg.take_loss() / ((args.steps + args.warmup + 2) * args.batch)
         sg.close()
-    out = {'model': args.model, 'graph': args.graph, 'ms_per_step': el / args.steps * 1e3, 'loss': float(loss),
+    out = {'model': args.model, 'graph': args.graph, 'ms_per_step': el / args.steps * 1e3, 'loss': float(torch.as_tensor(loss).detach()),
            'n_users': args.n_users,
            'n_items': args.n_items, 'n_edges': args.n_edges, 'd': args.d, 'layers': args.layers,
            'adj_nnz': m.norm_adj.nnz, 'feat_nnz': feat_nnz,

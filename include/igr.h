@@ -219,10 +219,14 @@ int igr_spmm_push_f32(const igr_csr *g, int32_t d, const int64_t *rows, int64_t 
  * On the reverse graph, out = A^T G (+ G): igr_spmm_push_f32's result. */
 int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, int32_t *slot,
                     void *stream);
-/* bits |= the selected rows and all their neighbours (square graph): the rows
- * at which a batch's last layer reads the layer below it (the row_mask of that
- * layer and the col_mask of its reverse, igr_epilogue). bits: uint32[(n+31)/32]. */
-int igr_rowset_mark_neighbors(const igr_csr *g, int64_t n_sel, const int64_t *rows, uint32_t *bits, void *stream);
+/* bits |= every column of the selected rows, and the row ids themselves when
+ * self_mark (square graph): the rows at which a batch's last layer reads the
+ * layer below it (the row_mask of that layer and the col_mask of its reverse,
+ * igr_epilogue; trainer.py:537, model.py:4048-4049).  bits: uint32[(n_cols+31)/32].
+ * igr_bitmap_set: bits |= {idx[i]}. */
+int igr_rowset_mark_neighbors(const igr_csr *g, int64_t n_sel, const int64_t *rows, uint32_t *bits,
+                              int32_t self_mark, void *stream);
+int igr_bitmap_set(int64_t n, const int64_t *idx, uint32_t *bits, void *stream);
 int igr_rowset_sum_f32(int64_t n_sel, int32_t d, const int64_t *rows, const int32_t *slot, const float *src,
                        int64_t lds, float scale, float *agg, int64_t ld_agg, void *stream);
 int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint32_t *bits, const uint32_t *filter,

@@ -180,20 +180,28 @@ __global__ void rowset_mark_kernel(int64_t n, const int64_t *__restrict__ rows, 
     slot[r] = (int32_t)i;  // any one of a repeated row's positions
 }
 
-// bits |= {rows[i]} and every column of those rows (one wave per selected row)
+// bits |= every column of the selected rows (and the row ids themselves when
+// self_mark); one wave per selected row
 __global__ __launch_bounds__(256) void rowset_mark_neighbors_kernel(int64_t n, const int64_t *__restrict__ rows,
                                                                     const int64_t *__restrict__ row_ptr,
                                                                     const int32_t *__restrict__ col,
-                                                                    uint32_t *__restrict__ bits) {
+                                                                    uint32_t *__restrict__ bits, int self_mark) {
     const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;
     const int lane = threadIdx.x & 63;
     const int64_t r = rows[i];
-    if (lane == 0) atomicOr(bits + (r >> 5), 1u << (r & 31));
+    if (self_mark && lane == 0) atomicOr(bits + (r >> 5), 1u << (r & 31));
     for (int64_t p = row_ptr[r] + lane; p < row_ptr[r + 1]; p += 64) {
         const uint32_t c = (uint32_t)col[p];
         atomicOr(bits + (c >> 5), 1u << (c & 31));
     }
+}
+
+__global__ void bitmap_set_kernel(int64_t n, const int64_t *__restrict__ idx, uint32_t *__restrict__ bits) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t r = idx[i];
+    atomicOr(bits + (r >> 5), 1u << (r & 31));
 }
 
 __global__ void rowset_clear_kernel(int64_t n, const int64_t *__restrict__ rows, uint32_t *__restrict__ bits,
@@ -321,15 +329,27 @@ extern "C" int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bit
 }
 
 extern "C" int igr_rowset_mark_neighbors(const igr_csr *g, int64_t n_sel, const int64_t *rows, uint32_t *bits,
-                                         void *stream) {
+                                         int32_t self_mark, void *stream) {
     return guarded("igr_rowset_mark_neighbors", [&]() -> int {
         if (!g) return arg_error("igr_rowset_mark_neighbors", "graph is NULL");
         if (n_sel <= 0) return IGR_OK;
         if (!rows || !bits) return arg_error("igr_rowset_mark_neighbors", "NULL pointer");
-        if (g->n_rows != g->n_cols) return arg_error("igr_rowset_mark_neighbors", "graph must be square");
+        if (self_mark && g->n_rows != g->n_cols)
+            return arg_error("igr_rowset_mark_neighbors", "self_mark needs a square graph");
         hipLaunchKernelGGL(rowset_mark_neighbors_kernel, dim3(blocks_for(n_sel, 4)), dim3(256), 0,
-                           reinterpret_cast<hipStream_t>(stream), n_sel, rows, g->row_ptr, g->col_idx, bits);
+                           reinterpret_cast<hipStream_t>(stream), n_sel, rows, g->row_ptr, g->col_idx, bits,
+                           self_mark ? 1 : 0);
         return launch_status("igr_rowset_mark_neighbors");
+    });
+}
+
+extern "C" int igr_bitmap_set(int64_t n, const int64_t *idx, uint32_t *bits, void *stream) {
+    return guarded("igr_bitmap_set", [&]() -> int {
+        if (n <= 0) return IGR_OK;
+        if (!idx || !bits) return arg_error("igr_bitmap_set", "NULL pointer");
+        hipLaunchKernelGGL(bitmap_set_kernel, dim3(blocks_for(n, 256)), dim3(256), 0,
+                           reinterpret_cast<hipStream_t>(stream), n, idx, bits);
+        return launch_status("igr_bitmap_set");
     });
 }
 

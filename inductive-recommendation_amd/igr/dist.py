@@ -42,6 +42,14 @@ def sharded_side(n_users, n_items, replicate='auto'):
     return 'users' if replicate == 'items' else 'items'
 
 
+def _align32(ranges, n):
+    """Move the inner boundaries of contiguous ranges to multiples of 32, so a row
+    bitmap over the whole range can be handed to each piece as a word offset."""
+    b = [0] + [min(n, 32 * int(round(e / 32))) for _, e in ranges[:-1]] + [n]
+    b = list(np.maximum.accumulate(b))
+    return [(int(b[k]), int(b[k + 1])) for k in range(len(ranges))]
+
+
 def balanced_ranges(degree, world):
     """Contiguous cut of rows into `world` ranges with ~equal edge counts."""
     cum = np.concatenate([[0], np.cumsum(degree, dtype=np.int64)])
@@ -111,8 +119,8 @@ class BipartiteShard:
         self.item_chunks = max(1, int(C))
         # row chunks with ~equal nnz, cut on the GLOBAL item degrees so every rank
         # all-reduces the same row ranges
-        cuts = balanced_ranges(degree[n_users:], self.item_chunks)
-        col_bounds = [int(round(k * nu / self.item_tiles)) for k in range(self.item_tiles + 1)]
+        cuts = _align32(balanced_ranges(degree[n_users:], self.item_chunks), n_items)
+        col_bounds = [min(nu, 32 * int(round(k * nu / self.item_tiles / 32))) for k in range(self.item_tiles)] + [nu]
         self.chunks = []  # (r0, r1, [(graph, vals, c0, c1), ...])
         for r0, r1 in cuts:
             e0, e1 = int(rp2[r0]), int(rp2[r1])
@@ -153,7 +161,7 @@ class BipartiteShard:
         return out
 
     def layer(self, x_users, x_items, y_users=None, y_items=None, group=None, spmm=None, hook=None,
-              add_users=None, add_items=None, beta=0.0, pending=(), acc_users=None, acc_div=1.0):
+              add_users=None, add_items=None, beta=0.0, pending=(), acc_users=None, acc_div=1.0, masks=None):
         """One layer: returns (Y[U_k], Y[I]) with Y[I] all-reduced across ranks.
 
         With add_users / add_items: Y[U_k] += beta * add_users and every rank
@@ -163,22 +171,35 @@ class BipartiteShard:
         user-side SpMM (the item side needs only x_users).  acc_users: the
         user-side epilogue also does acc_users = (acc_users + Y[U_k]) / acc_div
         (the forward's running layer mean).
-        `spmm(g, x, vals, out, accumulate, add=None, beta=0.)` defaults to the
-        HIP kernel (the CPU gloo tests pass the oracle); `hook(i, 'start'|'end')`
-        brackets each SpMM launch (bench timing)."""
+        masks = (mode, user_bits, item_bits), bitmaps over local users / items:
+        mode 'row' computes only the marked output rows (the others are left
+        as they were), mode 'col' reads only the marked source rows (the others
+        must hold zeros) - dist_train's batch-row step.
+        `spmm(g, x, vals, out, accumulate, add=None, beta=0., row_mask=None,
+        col_mask=None)` defaults to the HIP kernel (the CPU gloo tests pass the
+        oracle); `hook(i, 'start'|'end')` brackets each SpMM launch (bench timing)."""
         hook = hook or (lambda i, ph: None)
         spmm = spmm or _hip_spmm
         if y_items is None:
             y_items = torch.empty(self.n_items, x_users.shape[1], dtype=torch.float32, device=x_users.device)
+        mode, mu, mi = masks if masks is not None else (None, None, None)
+
+        def mk(bits, first):  # the bitmap seen from index `first` on (a multiple of 32)
+            return None if bits is None else bits[first // 32:]
         works, i = [], 0
         for r0, r1, tiles in self.chunks:
             yk = y_items[r0:r1]
             for t, (g, v, c0, c1) in enumerate(tiles):
                 hook(i, 'start')
+                kw = {}
+                if mode == 'row':
+                    kw['row_mask'] = mk(mi, r0)
+                elif mode == 'col':
+                    kw['col_mask'] = mk(mu, c0)
                 if t == 0 and add_items is not None:
-                    spmm(g, x_users[c0:c1], v, yk, False, add=add_items[r0:r1], beta=beta)
+                    spmm(g, x_users[c0:c1], v, yk, False, add=add_items[r0:r1], beta=beta, **kw)
                 else:
-                    spmm(g, x_users[c0:c1], v, yk, t > 0)
+                    spmm(g, x_users[c0:c1], v, yk, t > 0, **kw)
                 hook(i, 'end')
                 i += 1
             if self.world > 1:
@@ -189,6 +210,10 @@ class BipartiteShard:
             w.wait()
         hook(i, 'start')
         kw = {} if acc_users is None else dict(acc=acc_users, acc_mode=2, acc_div=acc_div)
+        if mode == 'row':
+            kw['row_mask'] = mu
+        elif mode == 'col':
+            kw['col_mask'] = mi
         if add_users is not None:
             spmm(self.user_block, x_items, self.user_vals, y_users, False, add=add_users, beta=beta, **kw)
         else:
@@ -199,12 +224,14 @@ class BipartiteShard:
         return y_users, y_items
 
 
-def _hip_spmm(g, x, vals, out, accumulate, add=None, beta=0.0, acc=None, acc_mode=0, acc_div=1.0):
+def _hip_spmm(g, x, vals, out, accumulate, add=None, beta=0.0, acc=None, acc_mode=0, acc_div=1.0, row_mask=None,
+              col_mask=None):
     """out = A x (+ out if accumulate) (+ beta * add), and acc = out (mode 1) or
-    acc = (acc + out) / acc_div (mode 2), all in the SpMM epilogue."""
+    acc = (acc + out) / acc_div (mode 2), all in the SpMM epilogue; row_mask /
+    col_mask restrict the rows computed / the source rows read."""
     if accumulate:
         add, beta = out, 1.0
-    if add is None and acc is None:
+    if add is None and acc is None and row_mask is None and col_mask is None:
         return ops.spmm(g, x, vals, out=out)
     return ops.spmm(g, x, vals, out=out, epi=ops.epilogue(beta=beta, add=add, acc=acc, acc_mode=acc_mode,
-                                                          acc_div=acc_div))
+                                                          acc_div=acc_div, row_mask=row_mask, col_mask=col_mask))

@@ -165,6 +165,25 @@ class ShardedPropagate(torch.autograd.Function):
         return demb, dw, None, None, None
 
 
+def _batch_masks(model, rows_u, items_all):
+    """Bitmaps of the rows the batch-row layer reads one layer below (HIP path):
+    local users = rows_u + the local neighbours of every rank's batch items;
+    items = every rank's batch items + the item neighbours of every rank's batch
+    users (OR over ranks: an item's value is the sum of all ranks' partials, so
+    every rank must compute its partial wherever any rank reads it)."""
+    sh = model.shard
+    mu = ops.column_mask(sh.item_block, items_all, extra=rows_u)
+    mi = ops.column_mask(sh.user_block, rows_u, extra=items_all)
+    if model.world > 1:
+        allm = torch.empty(model.world * mi.numel(), dtype=mi.dtype, device=mi.device)
+        dist.all_gather_into_tensor(allm, mi, group=model.group)
+        allm = allm.view(model.world, -1)
+        mi = allm[0].clone()
+        for k in range(1, model.world):
+            mi.bitwise_or_(allm[k])
+    return mu, mi
+
+
 class ShardedPropagateRows(torch.autograd.Function):
     """rep at the local batch rows [users (local ids); items_b] with the LAST
     layer computed only there (the single-GPU ops.PropagateRows on the shard).
@@ -198,11 +217,16 @@ class ShardedPropagateRows(torch.autograd.Function):
         x = torch.empty(nk + I, d, dtype=torch.float32, device=emb.device)
         model.feat_spmm(fs.graph, emb, fvals, x)
         pend = [_allreduce(x[nk:], group, async_op=True)] if world > 1 else []
+        # the layer under the batch-row layer only where that layer reads it (HIP path)
+        masks = _batch_masks(model, rows_u, items_all) if (L > 1 and spmm is _hip_spmm) else None
+        ctx.masks = masks
         su = si = None
         bufs = [torch.empty_like(x), torch.empty_like(x)]
         for layer in range(L - 1):
             y = bufs[layer % 2]
-            sh.layer(x[:nk], x[nk:], y_users=y[:nk], y_items=y[nk:], group=group, spmm=spmm, pending=pend)
+            lm = ('row',) + masks if (masks is not None and layer == L - 2) else None
+            sh.layer(x[:nk], x[nk:], y_users=y[:nk], y_items=y[nk:], group=group, spmm=spmm, pending=pend,
+                     masks=lm)
             pend = []
             gu, gi = R.gather(x[:nk], rows_u), R.gather(x[nk:], items_b)
             su = gu if su is None else su.add_(gu)
@@ -254,8 +278,10 @@ class ShardedPropagateRows(torch.autograd.Function):
             bufs = [torch.empty_like(x), x]
             for layer in range(L - 1):
                 y = bufs[layer % 2]
+                # dX_{L-1} is zero off the batch masks: the first reverse layer reads only them
+                lm = ('col',) + ctx.masks if (ctx.masks is not None and layer == 0) else None
                 sh.layer(x[:nk], x[nk:], y_users=y[:nk], y_items=y[nk:], group=group, spmm=spmm,
-                         add_items=gi_dense, beta=1.0)
+                         add_items=gi_dense, beta=1.0, masks=lm)
                 R.scatter(y[:nk], rows_u, gu)
                 x = y
         demb = torch.empty(fs.graph.n_cols, gs.shape[1], dtype=torch.float32, device=gs.device)

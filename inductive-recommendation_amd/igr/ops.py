@@ -217,8 +217,22 @@ def neighbor_mask(adj, rows):
     """Bitmap of `rows` and all their neighbours in the square graph adj
     (igr_rowset_mark_neighbors): where a batch's last layer reads the layer below."""
     mask = torch.zeros((adj.n_rows + 31) // 32, dtype=torch.int32, device=rows.device)
-    L.call('igr_rowset_mark_neighbors', ctypes.byref(adj.csr), rows.numel(), _p(rows), _p(mask), _stream())
+    L.call('igr_rowset_mark_neighbors', ctypes.byref(adj.csr), rows.numel(), _p(rows), _p(mask), 1, _stream())
     return mask
+
+
+def column_mask(g, rows, extra=None, out=None):
+    """Bitmap over g's columns: the columns of `rows` (int64, may be empty), plus
+    the column ids in `extra` (int64 or None)."""
+    if out is None:
+        out = torch.zeros((g.n_cols + 31) // 32, dtype=torch.int32, device=g.device)
+    if rows is not None and rows.numel():
+        rows = rows.to(torch.int64).contiguous()
+        L.call('igr_rowset_mark_neighbors', ctypes.byref(g.csr), rows.numel(), _p(rows), _p(out), 0, _stream())
+    if extra is not None and extra.numel():
+        extra = extra.to(torch.int64).contiguous()
+        L.call('igr_bitmap_set', extra.numel(), _p(extra), _p(out), _stream())
+    return out
 
 
 def sddmm_dot(g: Graph, u, v, h=1, out=None):

@@ -16,10 +16,13 @@ from igr.dist import BipartiteShard, balanced_ranges
 from oracle import igr_oracle as O
 
 
-def oracle_spmm(g, x, vals, out, accumulate, add=None, beta=0.0, acc=None, acc_mode=0, acc_div=1.0):
+def oracle_spmm(g, x, vals, out, accumulate, add=None, beta=0.0, acc=None, acc_mode=0, acc_div=1.0, row_mask=None,
+                col_mask=None):
     """The rank-local SpMM restated on the CPU: out = A x (+ out) (+ beta add),
     acc = out (mode 1) / (acc + out) / acc_div (mode 2).  vals are by edge id
-    (a reverse graph carries the forward edge ids)."""
+    (a reverse graph carries the forward edge ids).  row_mask / col_mask are
+    ignored: every row computed and every source read is a superset (unmarked
+    rows are never read, unmarked sources hold zeros)."""
     h = g.host()
     v = vals.numpy() if h['edge_id'] is None else vals.numpy()[h['edge_id']]
     A = O.CSR(g.n_rows, g.n_cols, h['row_ptr'], h['col_idx'].astype(np.int64), v)

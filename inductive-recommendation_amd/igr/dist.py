@@ -22,6 +22,8 @@ two sides, so a caller whose items outnumber its users passes the pairs with
 their columns swapped (then 'users' below means the sharded side) -
 `sharded_side` / bench.py --replicate.
 """
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -196,10 +198,14 @@ class BipartiteShard:
                     kw['row_mask'] = mk(mi, r0)
                 elif mode == 'col':
                     kw['col_mask'] = mk(mu, c0)
-                if t == 0 and add_items is not None:
-                    spmm(g, x_users[c0:c1], v, yk, False, add=add_items[r0:r1], beta=beta, **kw)
-                else:
-                    spmm(g, x_users[c0:c1], v, yk, t > 0, **kw)
+                d = x_users.shape[1]
+                W = _col_width(d, (c1 - c0) * d * 4) if ITEM_SIDE_COL_SPLIT else d
+                for c in range(0, d, W):
+                    sl = slice(c, c + W)
+                    if t == 0 and add_items is not None:
+                        spmm(g, x_users[c0:c1, sl], v, yk[:, sl], False, add=add_items[r0:r1, sl], beta=beta, **kw)
+                    else:
+                        spmm(g, x_users[c0:c1, sl], v, yk[:, sl], t > 0, **kw)
                 hook(i, 'end')
                 i += 1
             if self.world > 1:
@@ -209,19 +215,37 @@ class BipartiteShard:
         for w in pending:
             w.wait()
         hook(i, 'start')
-        kw = {} if acc_users is None else dict(acc=acc_users, acc_mode=2, acc_div=acc_div)
-        if mode == 'row':
-            kw['row_mask'] = mu
-        elif mode == 'col':
-            kw['col_mask'] = mi
-        if add_users is not None:
-            spmm(self.user_block, x_items, self.user_vals, y_users, False, add=add_users, beta=beta, **kw)
-        else:
-            spmm(self.user_block, x_items, self.user_vals, y_users, False, **kw)
+        # wide rows whose item table outgrows the Infinity Cache (d = 256 at 1M
+        # items): two passes over 128-column halves, each gathering from a
+        # cache-sized slice (same sums, column by column)
+        d = x_items.shape[1]
+        W = _col_width(d, x_items.shape[0] * d * 4)
+        for c in range(0, d, W):
+            sl = slice(c, c + W)
+            kw = {} if acc_users is None else dict(acc=acc_users[:, sl], acc_mode=2, acc_div=acc_div)
+            if mode == 'row':
+                kw['row_mask'] = mu
+            elif mode == 'col':
+                kw['col_mask'] = mi
+            if add_users is not None:
+                spmm(self.user_block, x_items[:, sl], self.user_vals, y_users[:, sl], False,
+                     add=add_users[:, sl], beta=beta, **kw)
+            else:
+                spmm(self.user_block, x_items[:, sl], self.user_vals, y_users[:, sl], False, **kw)
         hook(i, 'end')
         for w in works:
             w.wait()
         return y_users, y_items
+
+
+ITEM_SIDE_COL_SPLIT = os.environ.get('IGR_ITEM_COL_SPLIT', '1') == '1'
+
+
+def _col_width(d, table_bytes):
+    """Column width per pass of a wide-row SpMM: 128 when d = 256 and the gathered
+    table outgrows the Infinity Cache, so each pass gathers from a slice half as
+    large (same sums, column by column); d otherwise."""
+    return 128 if (d == 256 and table_bytes > MALL_BYTES) else d
 
 
 def _hip_spmm(g, x, vals, out, accumulate, add=None, beta=0.0, acc=None, acc_mode=0, acc_div=1.0, row_mask=None,

@@ -324,6 +324,26 @@ def test_bipartite_shard_tiled_items():
     close(yu2.cpu().numpy(), y64[:U])
 
 
+def test_bipartite_shard_column_halves_at_d256(monkeypatch):
+    """d = 256 with tables beyond the Infinity Cache runs both sides as two
+    128-column passes (forced here on a small graph by shrinking the cache
+    size): bitwise the full-width result, and both match the oracle."""
+    from igr import dist as D
+    U, I, E, d = 3000, 400, 40000, 256
+    rng = np.random.default_rng(15)
+    pairs = np.stack([rng.integers(0, U, E), rng.integers(0, I, E)], 1)
+    x = rng.standard_normal((U + I, d)).astype(np.float32)
+    sh = D.BipartiteShard(pairs, U, I, 0, 1, DEV, item_tiles=2, item_chunks=2)
+    yu_full, yi_full = sh.layer(t(x[:U]), t(x[U:]))
+    monkeypatch.setattr(D, 'MALL_BYTES', 0)
+    assert D._col_width(d, 1) == 128
+    yu, yi = sh.layer(t(x[:U]), t(x[U:]))
+    assert torch.equal(yu, yu_full) and torch.equal(yi, yi_full)
+    y64 = O.spmm64(O.norm_adj(U, I, pairs), x)
+    close(yu.cpu().numpy(), y64[:U])
+    close(yi.cpu().numpy(), y64[U:], atol_row=2e-6)
+
+
 def test_fused_adam_matches_torch():
     from igr.optim import Adam
     rng = np.random.default_rng(15)

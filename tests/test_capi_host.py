@@ -32,6 +32,20 @@ def test_library_exports_every_declared_symbol():
     assert lib.igr_version() == 10000
 
 
+def test_binding_arity_matches_header():
+    """Every prototype in include/igr.h has as many parameters as its ctypes
+    argtypes entry (a parameter added to the C ABI but not to the binding would
+    shift every later argument)."""
+    txt = open(os.path.join(ROOT, 'include', 'igr.h')).read()
+    txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
+    protos = dict(re.findall(r'\b(igr_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;', txt, flags=re.S))
+    assert len(protos) == len(_lib.SIGNATURES)
+    for name, params in protos.items():
+        params = params.strip()
+        n = 0 if params in ('', 'void') else params.count(',') + 1
+        assert n == len(_lib.SIGNATURES[name][1]), (name, n, len(_lib.SIGNATURES[name][1]))
+
+
 def test_error_path_reports_message():
     with pytest.raises(_lib.IgrError, match='index out of range'):
         G.csr_from_coo(np.array([0, 5]), np.array([0, 0]), 3, 3)

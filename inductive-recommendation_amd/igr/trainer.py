@@ -43,15 +43,25 @@ def get_trainer(config, dataset, model):
     return trainer(config)
 
 
-def calculate_metrics(eval_data, rec_items, topks):
-    """trainer.py:115-144, vectorised: Precision/Recall/NDCG@k averaged over
-    users with a non-empty eval set."""
-    n_users, kmax = rec_items.shape
-    lens = np.array([len(x) for x in eval_data], dtype=np.int32)
+def eval_keys(eval_data, n_users, n_items):
+    """The eval lists as sorted (user * n_items + item) keys plus their lengths:
+    what calculate_metrics matches the ranking against (reusable across evals)."""
+    lens = np.array([len(x) for x in eval_data[:n_users]], dtype=np.int32)
     ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
-    flat = np.fromiter((i for x in eval_data for i in x), dtype=np.int64, count=int(ptr[-1]))
-    n_items = int(max(rec_items.max(initial=0), flat.max(initial=0)) + 1)
-    ev_keys = np.unique(np.repeat(np.arange(n_users, dtype=np.int64), lens) * n_items + flat)
+    flat = np.fromiter((i for x in eval_data[:n_users] for i in x), dtype=np.int64, count=int(ptr[-1]))
+    return np.unique(np.repeat(np.arange(n_users, dtype=np.int64), lens) * n_items + flat), lens
+
+
+def calculate_metrics(eval_data, rec_items, topks, keys=None):
+    """trainer.py:115-144, vectorised: Precision/Recall/NDCG@k averaged over
+    users with a non-empty eval set.  keys: eval_keys(eval_data, ...) computed
+    once (with n_items >= every item id in eval_data and rec_items)."""
+    n_users, kmax = rec_items.shape
+    if keys is None:
+        n_items = int(max(rec_items.max(initial=0),
+                          max((max(x) for x in eval_data[:n_users] if x), default=0)) + 1)
+        keys = eval_keys(eval_data, n_users, n_items) + (n_items,)
+    ev_keys, lens, n_items = keys
     rk = (np.arange(n_users, dtype=np.int64)[:, None] * n_items + rec_items).ravel()
     j = np.minimum(np.searchsorted(ev_keys, rk), max(len(ev_keys) - 1, 0))
     hit = (ev_keys[j] == rk).reshape(n_users, kmax).astype(np.float32) if len(ev_keys) else \
@@ -170,7 +180,13 @@ class BasicTrainer:
         return None
 
     def calculate_metrics(self, eval_data, rec_items):
-        return calculate_metrics(eval_data, rec_items, self.topks)
+        # the eval lists never change during training: their keys are built once
+        cache = self.__dict__.setdefault('_eval_keys', {})
+        n_items = max(int(self.dataset.n_items), int(rec_items.max(initial=0)) + 1)
+        key = (id(eval_data), len(eval_data), rec_items.shape[0], n_items)
+        if key not in cache:
+            cache[key] = eval_keys(eval_data, rec_items.shape[0], n_items) + (n_items,)
+        return calculate_metrics(eval_data, rec_items, self.topks, keys=cache[key])
 
     @torch.no_grad()
     def rank(self, val_or_test, banned_items=None):
@@ -184,12 +200,17 @@ class BasicTrainer:
         rep = self.model.get_rep()
         excl = None
         if val_or_test != 'train':
-            lists = self.dataset.train_data
-            if val_or_test == 'test':
-                lists = [a + b for a, b in zip(self.dataset.train_data, self.dataset.val_data)]
-            ptr, flat = _csr(lists, n_users)
-            excl = (torch.from_numpy(ptr.astype(np.int64)).to(self.device),
-                    torch.from_numpy(flat.astype(np.int32)).to(self.device))
+            # the exclusion lists never change during training: one device CSR per split
+            cache = self.__dict__.setdefault('_excl', {})
+            ck = (val_or_test, id(self.dataset.train_data), id(self.dataset.val_data), n_users)
+            if ck not in cache:
+                lists = self.dataset.train_data
+                if val_or_test == 'test':
+                    lists = [a + b for a, b in zip(self.dataset.train_data, self.dataset.val_data)]
+                ptr, flat = _csr(lists, n_users)
+                cache[ck] = (torch.from_numpy(ptr.astype(np.int64)).to(self.device),
+                             torch.from_numpy(flat.astype(np.int32)).to(self.device))
+            excl = cache[ck]
         kmax = max(self.topks)
         rec = []
         # test_batch_size bounds the reference's score matrix; rows are ranked

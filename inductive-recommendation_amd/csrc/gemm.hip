@@ -142,8 +142,10 @@ __global__ __launch_bounds__(256) void gemm128_f32_mfma(int64_t M, int64_t N, in
                                                         const float *__restrict__ bias, float *__restrict__ C,
                                                         int64_t ldc) {
     constexpr int IMG = (BT * KSTR > BKT * MSTR) ? BT * KSTR : BKT * MSTR;
-    __shared__ float As[2][IMG];
-    __shared__ float Bs[2][IMG];
+    // one allocation: the operand images, then (after the K loop) the C staging area over both
+    __shared__ float smem[2 * 2 * IMG];
+    float(*As)[IMG] = reinterpret_cast<float(*)[IMG]>(smem);
+    float(*Bs)[IMG] = reinterpret_cast<float(*)[IMG]>(smem + 2 * IMG);
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
     const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves, 64x64 each
@@ -208,8 +210,8 @@ __global__ __launch_bounds__(256) void gemm128_f32_mfma(int64_t M, int64_t N, in
     // two 16-lane halves of a store sit 16 banks apart), then writes whole 256-B
     // row segments with 16-B stores instead of 64-B pieces from 16 lanes.
     constexpr int CS = 68;
-    float *Ws = &As[0][0] + wave * 32 * CS;  // 4 x 8.5 KB within As/Bs (36 KB)
-    static_assert(4 * 32 * CS <= 2 * IMG * 2, "C staging must fit in As + Bs");
+    float *Ws = smem + wave * 32 * CS;  // 4 x 8.5 KB within the 36 KB of operand images
+    static_assert(4 * 32 * CS <= 2 * 2 * IMG, "C staging must fit in the operand images");
     const bool vec = (ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15u) == 0);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {

@@ -91,22 +91,28 @@ __device__ __forceinline__ void store_row1(const Epi &e, int64_t r, int f, float
 
 // Edge-weight policies (template argument W of the kernels): the weight of
 // CSR position p of row r with source column c.
+// drops(): the policy zeroes edges at run time (in-kernel dropout); the launch
+// then takes the MASK variant, whose zero-weight edges skip their row gather.
 struct W_One {  // rhs == NULL: unit weights
+    bool drops() const { return false; }
     __device__ __forceinline__ float operator()(int64_t, int, int) const { return 1.f; }
 };
 struct W_Val {  // rhs by edge id == CSR position
     const float *val;
+    bool drops() const { return false; }
     __device__ __forceinline__ float operator()(int64_t p, int, int) const { return ld_stream(val + p); }
 };
 struct W_ValEid {  // rhs by edge id, edge id = edge_id[p] (multigraph / reverse graph)
     const float *val;
     const int64_t *eid;
+    bool drops() const { return false; }
     __device__ __forceinline__ float operator()(int64_t p, int, int) const { return val[ld_stream(eid + p)]; }
 };
 struct W_ValHead {  // per-head rhs [nnz, h] by edge id (CSR position or edge_id[p]), head j
     const float *val;
     const int64_t *eid;
     int64_t h, j;
+    bool drops() const { return false; }
     __device__ __forceinline__ float operator()(int64_t p, int, int) const {
         return val[(eid ? ld_stream(eid + p) : p) * h + j];
     }
@@ -129,6 +135,7 @@ struct W_Scaled {
     uint64_t seed, offset;
     const int64_t *offset_dev;  // + *offset_dev (a device step counter: hipGraph replays draw fresh masks)
     int swap;
+    bool drops() const { return keep < 1.f; }
     __device__ __forceinline__ float operator()(int64_t, int c, int r) const {
         float w = rs ? rs[r] : 1.f;
         if (cs) w *= cs[c];
@@ -221,13 +228,16 @@ __device__ __forceinline__ float4 gather_round(float4 acc, const int (&cl)[NB], 
     return acc;
 }
 
-// (col, val) of CSR position p; with a column mask, masked-out columns come back as -1
+// (col, val) of CSR position p; with MASK, masked-out columns and zero-weight
+// edges come back as -1
 template <bool MASK, class W>
 __device__ __forceinline__ void load_pair(const int32_t *__restrict__ col, const W &wfn, int64_t p, int r,
                                           const uint32_t *__restrict__ cmask, int &c, float &w) {
     c = ld_stream(col + p);
     w = wfn(p, c, r);
-    if (MASK && !bit_set(cmask, c)) {
+    // a dropped edge (w == 0) adds an exact 0 (the accumulator is never -0), so
+    // skipping its gather leaves every sum bitwise unchanged
+    if (MASK && ((cmask && !bit_set(cmask, c)) || w == 0.f)) {
         c = -1;
         w = 0.f;
     }
@@ -428,7 +438,7 @@ static void launch_fast(const igr_csr *g, const float *x, int64_t ldx, const W &
     const int64_t row_blocks = (g->n_order + 4 * G - 1) / (4 * G);
     const int64_t blocks = chunk_blocks + row_blocks;
     if (blocks > 0) {
-        if (epi.col_mask)
+        if (epi.col_mask || wfn.drops())
             hipLaunchKernelGGL((spmm_main<D, W, true>), dim3((unsigned)blocks), dim3(256), 0, st, g->row_ptr,
                                g->col_idx, wfn, x, ldx, g->order, g->n_order, g->chunk_row, g->chunk_beg,
                                g->n_chunks, g->chunk_edges, ws, chunk_blocks, epi);

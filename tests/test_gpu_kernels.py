@@ -109,6 +109,31 @@ def test_spmm_deterministic():
         assert torch.equal(a, ops.spmm(g, x, t(v)))
 
 
+@pytest.mark.parametrize('d', [32, 64, 128])
+def test_spmm_scaled_dropout_bitwise_explicit_values(d):
+    """In-kernel dropout skips the gathers of dropped edges; the sums are bitwise
+    those of the same SpMM with the dropped edges' values written as 0 (forward and
+    reverse graph, split rows included)."""
+    g, _ = rand_graph(600, 400, 30000, seed=21, skew=True, split_threshold=64, chunk_edges=64)
+    assert g.n_split > 0
+    rng = np.random.default_rng(d)
+    rs = rng.random(600).astype(np.float32) + 0.5
+    cs = rng.random(400).astype(np.float32) + 0.5
+    keep, seed, off = 0.75, 5, 3
+    h = g.host()
+    row = np.repeat(np.arange(600), np.diff(h['row_ptr']))
+    col = h['col_idx'].astype(np.int64)
+    x = t(rng.standard_normal((400, d)).astype(np.float32))
+    w = ops.ScaledWeights(t(rs), t(cs), keep, seed, off)
+    u = ops.dropout_uniforms(g, seed, off)
+    assert 0 < int((torch.floor(keep + u) == 0).sum()) < g.nnz
+    vals = ops.edge_dropout(t(rs[row] * cs[col]), u, 1.0 - keep)  # forward edge ids = CSR positions
+    assert torch.equal(ops.spmm_scaled(g, x, w), ops.spmm(g, x, vals))
+    xr = t(rng.standard_normal((600, d)).astype(np.float32))
+    rg = g.reverse()
+    assert torch.equal(ops.spmm_scaled(rg, xr, w.transposed()), ops.spmm(rg, xr, vals))
+
+
 def test_spmm_linearity_large():
     """Size-independent property at 1M edges: A(x1 + 2 x2) = A x1 + 2 A x2."""
     g, v = rand_graph(200000, 50000, 1000000, seed=17)

@@ -163,7 +163,8 @@ class BipartiteShard:
         return out
 
     def layer(self, x_users, x_items, y_users=None, y_items=None, group=None, spmm=None, hook=None,
-              add_users=None, add_items=None, beta=0.0, pending=(), acc_users=None, acc_div=1.0, masks=None):
+              add_users=None, add_items=None, beta=0.0, pending=(), acc_users=None, acc_div=1.0, masks=None,
+              defer=False):
         """One layer: returns (Y[U_k], Y[I]) with Y[I] all-reduced across ranks.
 
         With add_users / add_items: Y[U_k] += beta * add_users and every rank
@@ -179,7 +180,13 @@ class BipartiteShard:
         must hold zeros) - dist_train's batch-row step.
         `spmm(g, x, vals, out, accumulate, add=None, beta=0., row_mask=None,
         col_mask=None)` defaults to the HIP kernel (the CPU gloo tests pass the
-        oracle); `hook(i, 'start'|'end')` brackets each SpMM launch (bench timing)."""
+        oracle); `hook(i, 'start'|'end')` brackets each SpMM launch (bench timing).
+        defer: do not wait for this layer's item all-reduces; returns
+        (Y[U_k], Y[I], works) instead, and the caller passes `works` as the next
+        layer's `pending` - chained layers (x_{l+1} = y_l) then overlap the
+        reduce of layer l with the item-side SpMM of layer l+1 as well as with
+        the user side of layer l (Y[I] is complete only after the wait, and the
+        next layer must write its items into another buffer)."""
         hook = hook or (lambda i, ph: None)
         spmm = spmm or _hip_spmm
         if y_items is None:
@@ -233,9 +240,26 @@ class BipartiteShard:
             else:
                 spmm(self.user_block, x_items[:, sl], self.user_vals, y_users[:, sl], False, **kw)
         hook(i, 'end')
+        if defer:
+            return y_users, y_items, works
         for w in works:
             w.wait()
         return y_users, y_items
+
+    def propagate(self, x_users, x_items, n_layers, group=None, spmm=None):
+        """n_layers chained layers (x_{l+1} = A x_l, LightGCN's get_rep without
+        the mean) with each layer's item reduce deferred into the next layer;
+        returns the last (Y[U_k], Y[I]), fully reduced."""
+        d = x_users.shape[1]
+        bu = [torch.empty(self.u1 - self.u0, d, dtype=torch.float32, device=x_users.device) for _ in range(2)]
+        bi = [torch.empty(self.n_items, d, dtype=torch.float32, device=x_users.device) for _ in range(2)]
+        xu, xi, pend = x_users, x_items, []
+        for layer in range(n_layers):
+            xu, xi, pend = self.layer(xu, xi, bu[layer % 2], bi[layer % 2], group=group, spmm=spmm,
+                                      pending=pend, defer=True)
+        for w in pend:
+            w.wait()
+        return xu, xi
 
 
 ITEM_SIDE_COL_SPLIT = os.environ.get('IGR_ITEM_COL_SPLIT', '1') == '1'

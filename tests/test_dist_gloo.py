@@ -49,7 +49,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, pairs, U, I, d, q, tiles=1, chunks='auto'):
+def _worker(rank, world, port, pairs, U, I, d, q, tiles=1, chunks='auto', layers=1):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
@@ -59,7 +59,10 @@ def _worker(rank, world, port, pairs, U, I, d, q, tiles=1, chunks='auto'):
         g = torch.Generator().manual_seed(0)
         xu_all = torch.randn(U, d, generator=g)
         xi = torch.randn(I, d, generator=g)
-        yu, yi = sh.layer(xu_all[sh.u0:sh.u1].contiguous(), xi, spmm=oracle_spmm)
+        if layers == 1:
+            yu, yi = sh.layer(xu_all[sh.u0:sh.u1].contiguous(), xi, spmm=oracle_spmm)
+        else:  # chained layers, each item reduce deferred into the next layer
+            yu, yi = sh.propagate(xu_all[sh.u0:sh.u1].contiguous(), xi, layers, spmm=oracle_spmm)
         q.put((rank, sh.u0, sh.u1, yu.numpy(), yi.numpy(), sh.local_nnz))
     except Exception:
         import traceback
@@ -107,6 +110,35 @@ def test_sharded_layer_matches_unsharded(world, tiles, chunks):
         np.testing.assert_allclose(yu, y64[u0:u1], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(yi, y64[U:], rtol=1e-5, atol=1e-6)  # every rank holds the reduced items
     assert res[0][1] == 0 and res[-1][2] == U
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_chained_layers_with_deferred_reduces(world):
+    """BipartiteShard.propagate: three chained layers, each layer's item all-reduce
+    waited only by the next layer's user side == (D^-1/2 A D^-1/2)^3 x unsharded."""
+    U, I, E, d, L = 300, 120, 4000, 8, 3
+    rng = np.random.default_rng(5)
+    pairs = np.stack([rng.integers(0, U, E), rng.integers(0, I, E)], 1)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, pairs, U, I, d, q, 2, 2, L)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    errs = [r[2] for r in res if r[1] == 'error']
+    assert not errs, errs[0]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    A = O.norm_adj(U, I, pairs)
+    g = torch.Generator().manual_seed(0)
+    y = torch.cat([torch.randn(U, d, generator=g), torch.randn(I, d, generator=g)]).numpy().astype(np.float64)
+    for _ in range(L):
+        y = O.spmm64(A, y)
+    for rank, u0, u1, yu, yi, _ in res:
+        np.testing.assert_allclose(yu, y[u0:u1], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(yi, y[U:], rtol=1e-5, atol=1e-6)
 
 
 def test_item_chunks_identical_across_ranks():

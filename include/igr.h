@@ -214,7 +214,9 @@ int igr_spmm_push_f32(const igr_csr *g, int32_t d, const int64_t *rows, int64_t 
  *                     (one lane group per row, fixed order: deterministic
  *                     for distinct rows; repeats are summed into their slot
  *                     with float atomics).  Persistent 1024-thread workgroups
- *                     keep the 64 KB filter in LDS; only filter hits probe bits
+ *                     keep the 64 KB filter in LDS; only filter hits probe bits.
+ *                     row_mask (or NULL = every row): rows c with their bit
+ *                     clear are not computed and out[c] is left untouched
  *   igr_rowset_clear: zero the words of bits and filter holding the selected rows
  * On the reverse graph, out = A^T G (+ G): igr_spmm_push_f32's result. */
 int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, int32_t *slot,
@@ -231,7 +233,7 @@ int igr_rowset_sum_f32(int64_t n_sel, int32_t d, const int64_t *rows, const int3
                        int64_t lds, float scale, float *agg, int64_t ld_agg, void *stream);
 int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint32_t *bits, const uint32_t *filter,
                              const int32_t *slot, const float *agg, int64_t ld_agg, const float *rhs, float scale,
-                             int32_t self_add, float *out, int64_t ldo, void *stream);
+                             int32_t self_add, const uint32_t *row_mask, float *out, int64_t ldo, void *stream);
 int igr_rowset_clear(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, void *stream);
 
 /* Eval ranking (BasicTrainer.eval, trainer.py:146-182): scores of a user batch

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(1024) void spmm_pull_marked_kernel(
     int64_t n_rows, const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
     const float *__restrict__ val, const uint32_t *__restrict__ bits, const uint32_t *__restrict__ filter,
     int exact_filter, const int32_t *__restrict__ slot, const float *__restrict__ agg, int64_t ld_agg,
-    float *__restrict__ out, int64_t ldo, float scale, int self_add) {
+    float *__restrict__ out, int64_t ldo, float scale, int self_add, const uint32_t *__restrict__ row_mask) {
     constexpr int LPR = D / 4;  // lanes per row, one float4 each
     constexpr int RPB = 1024 / LPR;  // rows per workgroup pass
     constexpr int U = 4;  // blocks of LPR edges per trip (independent loads in flight)
@@ -244,7 +244,8 @@ __global__ __launch_bounds__(1024) void spmm_pull_marked_kernel(
     // persistent: the grid strides over row passes (every wave runs the same trip count)
     for (int64_t r0 = (int64_t)blockIdx.x * RPB; r0 < n_rows; r0 += (int64_t)gridDim.x * RPB) {
         const int64_t r = r0 + threadIdx.x / LPR;
-        const bool live = r < n_rows;
+        // rows outside row_mask are neither read nor written (trip count 0)
+        const bool live = r < n_rows && (!row_mask || ((row_mask[r >> 5] >> (r & 31)) & 1u));
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         int64_t b = 0, e = 0;
         if (live) {
@@ -379,7 +380,8 @@ extern "C" int igr_rowset_sum_f32(int64_t n_sel, int32_t d, const int64_t *rows,
 
 extern "C" int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint32_t *bits, const uint32_t *filter,
                                         const int32_t *slot, const float *agg, int64_t ld_agg, const float *rhs,
-                                        float scale, int32_t self_add, float *out, int64_t ldo, void *stream) {
+                                        float scale, int32_t self_add, const uint32_t *row_mask, float *out,
+                                        int64_t ldo, void *stream) {
     return guarded("igr_spmm_pull_marked_f32", [&]() -> int {
         const char *fn = "igr_spmm_pull_marked_f32";
         if (!g || !bits || !filter || !slot) return arg_error(fn, "graph / bits / filter / slot NULL");
@@ -404,7 +406,7 @@ extern "C" int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint3
     hipLaunchKernelGGL((spmm_pull_marked_kernel<DD>),                                                             \
                        dim3((unsigned)std::min<int64_t>(2 * (int64_t)cus, blocks_for(n, 1024 / (DD / 4)))),       \
                        dim3(1024), 0, st, n, g->row_ptr, g->col_idx, rhs, bits, filter, exact, slot, agg, ld_agg, \
-                       out, ldo, scale, (int)self_add)
+                       out, ldo, scale, (int)self_add, row_mask)
         switch (d) {
             case 32: IGR_PULL(32); break;
             case 64: IGR_PULL(64); break;

@@ -5,7 +5,9 @@
 //                            trainer.py:522-535)
 //   igr_adam_f32            fused Adam update, torch.optim.Adam    trainer.py:44-46, 555
 //                           semantics in one pass
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -62,6 +64,11 @@ __global__ void bpr_sample_kernel(int64_t batch, int64_t n_active, const int32_t
 // torch forms them from Python floats.
 // step_dev (hipGraph-capturable form): the step is step0 + *step_dev, read on the
 // device, and the bias corrections are formed from it in double here.
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4f to_v4(float4 a) { return v4f{a.x, a.y, a.z, a.w}; }
+__device__ __forceinline__ float4 from_v4(v4f a) { return make_float4(a.x, a.y, a.z, a.w); }
+
+template <int U, bool NT>
 __global__ void adam_kernel(int64_t n, float *__restrict__ p, const float *__restrict__ g,
                             float *__restrict__ m, float *__restrict__ v, float omb1, float b2, float omb2,
                             float eps, float wd, float step_size, float bc2_sqrt,
@@ -74,23 +81,43 @@ __global__ void adam_kernel(int64_t n, float *__restrict__ p, const float *__res
     }
     const int64_t n4 = n >> 2;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-        float4 pp = reinterpret_cast<float4 *>(p)[i];
-        float4 gg = reinterpret_cast<const float4 *>(g)[i];
-        float4 mm = reinterpret_cast<float4 *>(m)[i];
-        float4 vv = reinterpret_cast<float4 *>(v)[i];
-        float *pa = &pp.x, *ga = &gg.x, *ma = &mm.x, *va = &vv.x;
+    // U float4 of each array per thread per trip, all loads issued before the math
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4; i0 += stride * U) {
+        float4 pp[U], gg[U], mm[U], vv[U];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float gk = wd != 0.f ? ga[k] + wd * pa[k] : ga[k];
-            ma[k] = ma[k] + omb1 * (gk - ma[k]);
-            va[k] = va[k] * b2 + omb2 * gk * gk;
-            const float den = sqrtf(va[k]) / bc2_sqrt + eps;
-            pa[k] = pa[k] - step_size * (ma[k] / den);
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i < n4) {
+                pp[u] = reinterpret_cast<float4 *>(p)[i];
+                gg[u] = NT ? from_v4(__builtin_nontemporal_load(reinterpret_cast<const v4f *>(g) + i))
+                           : reinterpret_cast<const float4 *>(g)[i];
+                mm[u] = reinterpret_cast<float4 *>(m)[i];
+                vv[u] = reinterpret_cast<float4 *>(v)[i];
+            }
         }
-        reinterpret_cast<float4 *>(p)[i] = pp;
-        reinterpret_cast<float4 *>(m)[i] = mm;
-        reinterpret_cast<float4 *>(v)[i] = vv;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i >= n4) break;
+            float *pa = &pp[u].x, *ga = &gg[u].x, *ma = &mm[u].x, *va = &vv[u].x;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float gk = wd != 0.f ? ga[k] + wd * pa[k] : ga[k];
+                ma[k] = ma[k] + omb1 * (gk - ma[k]);
+                va[k] = va[k] * b2 + omb2 * gk * gk;
+                const float den = sqrtf(va[k]) / bc2_sqrt + eps;
+                pa[k] = pa[k] - step_size * (ma[k] / den);
+            }
+            if (NT) {
+                __builtin_nontemporal_store(to_v4(pp[u]), reinterpret_cast<v4f *>(p) + i);
+                __builtin_nontemporal_store(to_v4(mm[u]), reinterpret_cast<v4f *>(m) + i);
+                __builtin_nontemporal_store(to_v4(vv[u]), reinterpret_cast<v4f *>(v) + i);
+            } else {
+                reinterpret_cast<float4 *>(p)[i] = pp[u];
+                reinterpret_cast<float4 *>(m)[i] = mm[u];
+                reinterpret_cast<float4 *>(v)[i] = vv[u];
+            }
+        }
     }
     for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const float gk = wd != 0.f ? g[i] + wd * p[i] : g[i];
@@ -141,9 +168,30 @@ extern "C" int igr_adam_f32(int64_t n, float *param, const float *grad, float *e
         const float bc2_sqrt = (float)std::sqrt(bc2);
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         const float omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2);
-        hipLaunchKernelGGL(adam_kernel, dim3(grid_for((n + 3) / 4, 256)), dim3(256), 0, st, n, param, grad,
-                           exp_avg, exp_avg_sq, omb1, (float)beta2, omb2, (float)eps, (float)weight_decay, step_size, bc2_sqrt,
-                           step_dev, step, lr, beta1, beta2);
+        // one float4 of each array per thread (no grid cap) with non-temporal
+        // traffic: 5.15 -> 5.7 TB/s on the 70 M-parameter table
+        // (scripts/tune_adam.py, profiles/r01m_adam_sweep.json); the knobs
+        // IGR_ADAM_U (float4s per thread per trip), IGR_ADAM_GRID (> 0: cap)
+        // and IGR_ADAM_NT are read per call for that sweep
+        const char *eu = getenv("IGR_ADAM_U");
+        const char *eg = getenv("IGR_ADAM_GRID");
+        const char *en = getenv("IGR_ADAM_NT");
+        const int U = eu ? atoi(eu) : 1;
+        const bool nt = en ? atoi(en) == 1 : true;
+        int64_t grid = std::min<int64_t>(((n + 3) / 4 + 255) / 256, int64_t(1) << 30);
+        if (eg && atoi(eg) > 0) grid = std::min<int64_t>(grid, atoi(eg));
+        grid = std::max<int64_t>(grid, 1);
+#define IGR_ADAM(UU)                                                                                             \
+    if (nt) hipLaunchKernelGGL((adam_kernel<UU, true>), dim3((unsigned)grid), dim3(256), 0, st, n, param, grad,      \
+                               exp_avg, exp_avg_sq, omb1, (float)beta2, omb2, (float)eps, (float)weight_decay,      \
+                               step_size, bc2_sqrt, step_dev, step, lr, beta1, beta2);                               \
+    else hipLaunchKernelGGL((adam_kernel<UU, false>), dim3((unsigned)grid), dim3(256), 0, st, n, param, grad, exp_avg, exp_avg_sq, \
+                       omb1, (float)beta2, omb2, (float)eps, (float)weight_decay, step_size, bc2_sqrt, step_dev, step,  \
+                       lr, beta1, beta2)
+        if (U == 4) IGR_ADAM(4);
+        else if (U == 2) IGR_ADAM(2);
+        else IGR_ADAM(1);
+#undef IGR_ADAM
         return launch_status("igr_adam_f32");
     });
 }

@@ -64,7 +64,7 @@ SIGNATURES = {
     'igr_bitmap_set': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp]),
     'igr_rowset_sum_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_f32, c_vp, c_i64, c_vp]),
     'igr_spmm_pull_marked_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32,
-                                                c_i32, c_vp, c_i64, c_vp]),
+                                                c_i32, c_vp, c_vp, c_i64, c_vp]),
     'igr_rowset_clear': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     'igr_mask_scores_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     'igr_topk_f32': (ctypes.c_int, [c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),

@@ -608,11 +608,13 @@ def _rowset(g: Graph):
     return rs
 
 
-def spmm_pull(g: Graph, rows, src, rhs=None, scale=1.0, self_add=False, out=None):
+def spmm_pull(g: Graph, rows, src, rhs=None, scale=1.0, self_add=False, out=None, row_mask=None):
     """out[c] = scale * (sum_{p in row c} rhs[p] S[col[p]] + self_add S[c]) with
     S[r] = sum of src[i] over rows[i] == r - the atomic-free equivalent of
-    spmm_push on the reverse graph (igr_spmm_pull_marked_f32)."""
-    _dev(src, rows, rhs, out)
+    spmm_push on the reverse graph (igr_spmm_pull_marked_f32).  row_mask (a
+    bitmap over the rows): only the marked rows are computed; the others of
+    `out` are left as they were."""
+    _dev(src, rows, rhs, out, row_mask)
     if g.edge_id is not None and rhs is not None:
         raise IgrError('spmm_pull: rhs by edge id needs a graph without an edge_id permutation')
     src, lds = _rows(src)
@@ -626,8 +628,8 @@ def spmm_pull(g: Graph, rows, src, rhs=None, scale=1.0, self_add=False, out=None
     L.call('igr_rowset_mark', rows.numel(), _p(rows), _p(bits), _p(filt), _p(slot), st)
     L.call('igr_rowset_sum_f32', rows.numel(), d, _p(rows), _p(slot), _p(src), lds, 1.0, _p(agg), agg.stride(0), st)
     L.call('igr_spmm_pull_marked_f32', ctypes.byref(g.csr), d, _p(bits), _p(filt), _p(slot), _p(agg), agg.stride(0),
-           _p(None if rhs is None else _f32(rhs).contiguous()), float(scale), int(bool(self_add)), _p(out),
-           out.stride(0), st)
+           _p(None if rhs is None else _f32(rhs).contiguous()), float(scale), int(bool(self_add)), _p(row_mask),
+           _p(out), out.stride(0), st)
     L.call('igr_rowset_clear', rows.numel(), _p(rows), _p(bits), _p(filt), st)
     return out
 
@@ -691,12 +693,14 @@ class PropagateRows(torch.autograd.Function):
         adj, feat, n_layers = ctx.adj, ctx.feat, ctx.L
         gs = gb.contiguous() / float(n_layers + 1)
         rs = _prescale(fvals) if feat is not None else None
+        mask = ctx.mask
         if adj.reverse() is adj:
-            dx = spmm_pull(adj, rows, gs, adj_vals, self_add=True)
+            # with L > 1, dx_{L-1} is read only through the first reverse layer's
+            # column mask (the neighbour set R): rows off R are not computed
+            dx = spmm_pull(adj, rows, gs, adj_vals, self_add=True, row_mask=mask if n_layers > 1 else None)
         else:
             dx = torch.zeros(adj.n_cols, gs.shape[1], dtype=torch.float32, device=gs.device)
             spmm_push(adj, rows, gs, dx, adj_vals, self_add=True)
-        mask = ctx.mask
         if n_layers > 1:
             at = adj.reverse()
             nxt = torch.empty_like(dx)

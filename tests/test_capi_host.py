@@ -190,9 +190,9 @@ def test_new_entry_points_validate_arguments():
              match='edge_id')
     tall = G.Graph(np.array([0, 1, 2, 3]), np.array([0, 1, 0], np.int32), 3, 2, device='cpu')  # 3 x 2
     _refused('igr_spmm_push_f32', ctypes.byref(tall.csr), 64, F, 4, F, 64, None, 1.0, 1, F, 64, st, match='square')
-    _refused('igr_spmm_pull_marked_f32', ctypes.byref(rect.csr), 64, None, F, F, F, 64, None, 1.0, 0, F, 64, st,
+    _refused('igr_spmm_pull_marked_f32', ctypes.byref(rect.csr), 64, None, F, F, F, 64, None, 1.0, 0, None, F, 64, st,
              match='NULL')
-    _refused('igr_spmm_pull_marked_f32', ctypes.byref(multi.csr), 64, F, F, F, F, 64, F, 1.0, 0, F, 64, st,
+    _refused('igr_spmm_pull_marked_f32', ctypes.byref(multi.csr), 64, F, F, F, F, 64, F, 1.0, 0, None, F, 64, st,
              match='edge_id')
     _refused('igr_rowset_mark', 4, F, None, F, F, st, match='NULL')
     _refused('igr_rowset_sum_f32', 4, 64, F, F, F, 32, 1.0, F, 64, st, match='leading')

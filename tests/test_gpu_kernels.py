@@ -484,6 +484,19 @@ def test_spmm_pull_marked_equals_push(d):
         y1 = ops.spmm_pull(g, t(u), t(src[:len(u)]), t(vv), scale=0.5, self_add=True).cpu().numpy()
         y2 = ops.spmm_pull(g, t(u), t(src[:len(u)]), t(vv), scale=0.5, self_add=True).cpu().numpy()
         assert np.array_equal(y1, y2)
+        # row_mask: the rows' neighbour set is computed bitwise as without it,
+        # every other row of out is left untouched
+        us = u[u != 5][:3]  # a few non-hub rows: their neighbour set leaves most rows out
+        y1 = ops.spmm_pull(g, t(us), t(src[:len(us)]), t(vv), scale=0.5, self_add=True).cpu().numpy()
+        nb = ops.neighbor_mask(g, t(us))
+        sentinel = torch.full((n, d), 7.0, device=DEV)
+        y3 = ops.spmm_pull(g, t(us), t(src[:len(us)]), t(vv), scale=0.5, self_add=True, out=sentinel,
+                           row_mask=nb).cpu().numpy()
+        marked = np.zeros(n, bool)
+        marked[us] = True
+        marked[h['col_idx'][np.isin(erow, us)]] = True
+        np.testing.assert_array_equal(y3[marked], y1[marked])
+        assert (y3[~marked] == 7.0).all() and (~marked).any()
     bits, filt, _ = ops._rowset(g)
     assert int(bits.abs().sum()) == 0 and int(filt.abs().sum()) == 0
 

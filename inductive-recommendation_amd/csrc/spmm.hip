@@ -370,13 +370,13 @@ __global__ __launch_bounds__(256, IGR_SPMM_MIN_WAVES) void spmm_main(
 // order, then the slots are added in a fixed tree through LDS, so the result
 // is the same on every run whatever the chunk count (a row of 10^6 edges has
 // ~2000 chunks; a single group would walk them serially).
-template <int D>
-__global__ __launch_bounds__(256) void spmm_combine(const int32_t *__restrict__ split_row,
-                                                    const int64_t *__restrict__ split_ptr,
-                                                    int64_t n_split, const float *__restrict__ ws,
-                                                    Epi epi) {
+template <int D, int NT>
+__global__ __launch_bounds__(NT) void spmm_combine(const int32_t *__restrict__ split_row,
+                                                   const int64_t *__restrict__ split_ptr,
+                                                   int64_t n_split, const float *__restrict__ ws,
+                                                   Epi epi) {
     constexpr int LPR = D / 4;
-    constexpr int S = 4 * (64 / LPR);  // slots per workgroup
+    constexpr int S = (NT / 64) * (64 / LPR);  // slots per workgroup
     __shared__ float4 red[S][LPR];
     const int slot = threadIdx.x / LPR;
     const int sub = threadIdx.x - slot * LPR;
@@ -447,9 +447,17 @@ static void launch_fast(const igr_csr *g, const float *x, int64_t ldx, const W &
                                g->col_idx, wfn, x, ldx, g->order, g->n_order, g->chunk_row, g->chunk_beg,
                                g->n_chunks, g->chunk_edges, ws, chunk_blocks, epi);
     }
-    if (g->n_split > 0)
-        hipLaunchKernelGGL((spmm_combine<D>), dim3((unsigned)g->n_split), dim3(256), 0, st, g->split_row,
-                           g->split_ptr, g->n_split, ws, epi);
+    if (g->n_split > 0) {
+        // rows of ~64+ chunks on average (the feature graph's general rows: 10^3-10^4
+        // chunks) take 1024-thread workgroups, 4x the partial loads in flight;
+        // the choice depends on the graph only, so results stay reproducible
+        if (g->n_chunks >= 64 * g->n_split)
+            hipLaunchKernelGGL((spmm_combine<D, 1024>), dim3((unsigned)g->n_split), dim3(1024), 0, st, g->split_row,
+                               g->split_ptr, g->n_split, ws, epi);
+        else
+            hipLaunchKernelGGL((spmm_combine<D, 256>), dim3((unsigned)g->n_split), dim3(256), 0, st, g->split_row,
+                               g->split_ptr, g->n_split, ws, epi);
+    }
 }
 
 // Validate the epilogue / shapes, pick the fast (d in {32,64,128,256}, 16-B

@@ -134,6 +134,24 @@ def test_spmm_scaled_dropout_bitwise_explicit_values(d):
     assert torch.equal(ops.spmm_scaled(rg, xr, w.transposed()), ops.spmm(rg, xr, vals))
 
 
+@pytest.mark.parametrize('d', [32, 64, 128, 256])
+def test_spmm_hub_rows_wide_combine(d):
+    """Split rows averaging >= 64 chunks (the feature graph's general rows) are
+    combined by 1024-thread workgroups: oracle parity, run-to-run bitwise."""
+    rng = np.random.default_rng(d)
+    n_rows, n_cols = 300, 4000
+    row = np.concatenate([np.zeros(20000, np.int64), np.full(9000, 7), rng.integers(0, n_rows, 3000)])
+    col = rng.integers(0, n_cols, len(row))
+    val = rng.standard_normal(len(row)).astype(np.float32)
+    g, v = G.Graph.from_coo(row, col, n_rows, n_cols, val, dedup=False, device=DEV, split_threshold=64,
+                            chunk_edges=64)
+    assert g.n_split >= 2 and g.n_chunks >= 64 * g.n_split
+    x = rng.standard_normal((n_cols, d)).astype(np.float32)
+    y = ops.spmm(g, t(x), t(v))
+    close(y.cpu().numpy(), O.spmm64(oracle_csr(g, v), x))
+    assert torch.equal(y, ops.spmm(g, t(x), t(v)))
+
+
 def test_spmm_linearity_large():
     """Size-independent property at 1M edges: A(x1 + 2 x2) = A x1 + 2 A x2."""
     g, v = rand_graph(200000, 50000, 1000000, seed=17)

@@ -225,9 +225,11 @@ int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t
  * self_mark (square graph): the rows at which a batch's last layer reads the
  * layer below it (the row_mask of that layer and the col_mask of its reverse,
  * igr_epilogue; trainer.py:537, model.py:4048-4049).  bits: uint32[(n_cols+31)/32].
+ * scratch: NULL (atomic bit marks) or uint8[n_cols] of zeros, 16-byte aligned
+ * (byte marks packed into bits afterwards; left zero again).
  * igr_bitmap_set: bits |= {idx[i]}. */
 int igr_rowset_mark_neighbors(const igr_csr *g, int64_t n_sel, const int64_t *rows, uint32_t *bits,
-                              int32_t self_mark, void *stream);
+                              int32_t self_mark, uint8_t *scratch, void *stream);
 int igr_bitmap_set(int64_t n, const int64_t *idx, uint32_t *bits, void *stream);
 int igr_rowset_sum_f32(int64_t n_sel, int32_t d, const int64_t *rows, const int32_t *slot, const float *src,
                        int64_t lds, float scale, float *agg, int64_t ld_agg, void *stream);

@@ -60,7 +60,7 @@ SIGNATURES = {
     'igr_spmm_push_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_f32, c_i32, c_vp,
                                          c_i64, c_vp]),
     'igr_rowset_mark': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    'igr_rowset_mark_neighbors': (ctypes.c_int, [_P(IgrCsr), c_i64, c_vp, c_vp, c_i32, c_vp]),
+    'igr_rowset_mark_neighbors': (ctypes.c_int, [_P(IgrCsr), c_i64, c_vp, c_vp, c_i32, c_vp, c_vp]),
     'igr_bitmap_set': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp]),
     'igr_rowset_sum_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_f32, c_vp, c_i64, c_vp]),
     'igr_spmm_pull_marked_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32,

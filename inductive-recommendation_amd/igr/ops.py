@@ -217,8 +217,18 @@ def neighbor_mask(adj, rows):
     """Bitmap of `rows` and all their neighbours in the square graph adj
     (igr_rowset_mark_neighbors): where a batch's last layer reads the layer below."""
     mask = torch.zeros((adj.n_rows + 31) // 32, dtype=torch.int32, device=rows.device)
-    L.call('igr_rowset_mark_neighbors', ctypes.byref(adj.csr), rows.numel(), _p(rows), _p(mask), 1, _stream())
+    L.call('igr_rowset_mark_neighbors', ctypes.byref(adj.csr), rows.numel(), _p(rows), _p(mask), 1,
+           _p(_mark_scratch(adj)), _stream())
     return mask
+
+
+def _mark_scratch(g):
+    """Per-graph uint8[n_cols] byte map for igr_rowset_mark_neighbors (zero between uses)."""
+    s = getattr(g, '_mark_bytes', None)
+    if s is None:
+        s = torch.zeros(max(g.n_cols, 1) + 16, dtype=torch.uint8, device=g.device)
+        g._mark_bytes = s
+    return s
 
 
 def column_mask(g, rows, extra=None, out=None):
@@ -228,7 +238,8 @@ def column_mask(g, rows, extra=None, out=None):
         out = torch.zeros((g.n_cols + 31) // 32, dtype=torch.int32, device=g.device)
     if rows is not None and rows.numel():
         rows = rows.to(torch.int64).contiguous()
-        L.call('igr_rowset_mark_neighbors', ctypes.byref(g.csr), rows.numel(), _p(rows), _p(out), 0, _stream())
+        L.call('igr_rowset_mark_neighbors', ctypes.byref(g.csr), rows.numel(), _p(rows), _p(out), 0,
+               _p(_mark_scratch(g)), _stream())
     if extra is not None and extra.numel():
         extra = extra.to(torch.int64).contiguous()
         L.call('igr_bitmap_set', extra.numel(), _p(extra), _p(out), _stream())

@@ -152,6 +152,38 @@ def test_spmm_hub_rows_wide_combine(d):
     assert torch.equal(y, ops.spmm(g, t(x), t(v)))
 
 
+def _bits_to_bool(bits, n):
+    b = bits.cpu().numpy().view(np.uint32)
+    return ((b[np.arange(n) >> 5] >> (np.arange(n) & 31).astype(np.uint32)) & 1).astype(bool)
+
+
+def test_neighbor_and_column_masks_byte_map():
+    """igr_rowset_mark_neighbors through the byte map (packed, scratch re-zeroed)
+    == the set restated in numpy == the atomic-bit path; n not a multiple of 32,
+    repeated rows, two calls with different rows."""
+    import ctypes
+    n = 1000 + 13
+    g, _ = rand_graph(n, n, 30000, seed=31)
+    h = g.host()
+    erow = np.repeat(np.arange(n), np.diff(h['row_ptr']))
+    rng = np.random.default_rng(2)
+    for trial in range(2):
+        rows = rng.integers(0, n, 40)
+        rows[:5] = rows[5]
+        for self_mark in (True, False):
+            want = np.zeros(n, bool)
+            want[h['col_idx'][np.isin(erow, rows)]] = True
+            if self_mark:
+                want[rows] = True
+            got = ops.neighbor_mask(g, t(rows)) if self_mark else ops.column_mask(g, t(rows))
+            np.testing.assert_array_equal(_bits_to_bool(got, n), want)
+            atomic = torch.zeros((n + 31) // 32, dtype=torch.int32, device=DEV)
+            ops.L.call('igr_rowset_mark_neighbors', ctypes.byref(g.csr), len(rows), ops._p(t(rows)), ops._p(atomic),
+                       int(self_mark), None, ops._stream())
+            assert torch.equal(atomic, got)
+        assert int(ops._mark_scratch(g).sum()) == 0
+
+
 def test_spmm_linearity_large():
     """Size-independent property at 1M edges: A(x1 + 2 x2) = A x1 + 2 A x2."""
     g, v = rand_graph(200000, 50000, 1000000, seed=17)

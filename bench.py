@@ -141,11 +141,9 @@ def main():
     dev = torch.device('cuda', dev_index)
     if world > 1:
         if args.dist_backend == 'nccl':
-            # RCCL over xGMI, its kernels on a high-priority stream so the item
-            # all-reduces progress while the SpMM grid fills the chip
-            opts = dist.ProcessGroupNCCL.Options()
-            opts.is_high_priority_stream = True
-            dist.init_process_group('nccl', device_id=dev, pg_options=opts)
+            # RCCL over xGMI; its stream stays at the default priority (streams of
+            # different priorities have hung on these machines)
+            dist.init_process_group('nccl', device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
 
@@ -234,14 +232,15 @@ def main():
     exposed_ms += ev[-1][nl - 1][1].elapsed_time(ev_done) / args.steps
     compute_ms = float(kern_ms.sum(1).mean())
 
-    stats = torch.tensor([elapsed, float(shard.local_nnz)], dtype=torch.float64, device=dev)
     if world > 1:
-        t = stats[:1].clone()
+        # RCCL reduces device tensors; a gloo rehearsal is only ever handed CPU tensors
+        sdev = dev if args.dist_backend == 'nccl' else torch.device('cpu')
+        t = torch.tensor([elapsed], dtype=torch.float64, device=sdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        n = stats[1:].clone()
+        n = torch.tensor([float(shard.local_nnz)], dtype=torch.float64, device=sdev)
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
         elapsed, total_nnz = float(t.item()), int(n.item())
-        ex = torch.tensor([exposed_ms, compute_ms], dtype=torch.float64, device=dev)
+        ex = torch.tensor([exposed_ms, compute_ms], dtype=torch.float64, device=sdev)
         dist.all_reduce(ex, op=dist.ReduceOp.MAX)
         exposed_ms, compute_ms = float(ex[0]), float(ex[1])
     else:

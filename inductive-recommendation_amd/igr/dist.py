@@ -26,9 +26,7 @@ import os
 
 import numpy as np
 import torch
-import torch.distributed as dist
-
-from . import ops
+from . import comm, ops
 from .graph import Graph, TiledGraph, csr_from_coo, sym_norm_values
 
 MALL_BYTES = 256 << 20  # MI355X Infinity Cache
@@ -216,7 +214,7 @@ class BipartiteShard:
                 hook(i, 'end')
                 i += 1
             if self.world > 1:
-                works.append(dist.all_reduce(yk, op=dist.ReduceOp.SUM, group=group, async_op=True))
+                works.append(comm.all_reduce_sum(yk, group, async_op=True))
         if y_users is None:
             y_users = torch.empty(self.u1 - self.u0, x_items.shape[1], dtype=torch.float32, device=x_items.device)
         for w in pending:

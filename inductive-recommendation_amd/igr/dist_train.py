@@ -36,17 +36,16 @@ the oracle; on a GPU it is the HIP kernel.
 """
 import numpy as np
 import torch
-import torch.distributed as dist
 import torch.nn as nn
 
-from . import ops
+from . import comm, ops
 from .dist import BipartiteShard, _hip_spmm
 from .graph import Graph, csr_from_coo
 from .model import train_pairs
 
 
 def _allreduce(t, group, async_op=False):
-    return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    return comm.all_reduce_sum(t, group, async_op=async_op)
 
 
 class FeatureShard:
@@ -176,7 +175,7 @@ def _batch_masks(model, rows_u, items_all):
     mi = ops.column_mask(sh.user_block, rows_u, extra=items_all)
     if model.world > 1:
         allm = torch.empty(model.world * mi.numel(), dtype=mi.dtype, device=mi.device)
-        dist.all_gather_into_tensor(allm, mi, group=model.group)
+        comm.all_gather_into(allm, mi, model.group)
         allm = allm.view(model.world, -1)
         mi = allm[0].clone()
         for k in range(1, model.world):
@@ -210,7 +209,7 @@ class ShardedPropagateRows(torch.autograd.Function):
         world = model.world
         if world > 1:
             items_all = torch.empty(world * items_b.numel(), dtype=torch.int64, device=emb.device)
-            dist.all_gather_into_tensor(items_all, items_b, group=group)
+            comm.all_gather_into(items_all, items_b, group)
         else:
             items_all = items_b
         ctx.save_for_backward(emb if aux is not None else None, w, rows_u, items_b, items_all)
@@ -262,7 +261,7 @@ class ShardedPropagateRows(torch.autograd.Function):
         gu, gi = gs[:B], gs[B:]
         if model.world > 1:
             gi_all = torch.empty(model.world * gi.shape[0], gi.shape[1], dtype=gi.dtype, device=gi.device)
-            dist.all_gather_into_tensor(gi_all, gi.contiguous(), group=group)
+            comm.all_gather_into(gi_all, gi.contiguous(), group)
         else:
             gi_all = gi
         x = torch.empty(nk + I, gs.shape[1], dtype=torch.float32, device=gs.device)

@@ -45,10 +45,7 @@ def main():
     if args.sharded and world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', '0')))
-        opts = dist.ProcessGroupNCCL.Options()
-        opts.is_high_priority_stream = True  # RCCL on a high-priority stream, as bench.py
-        dist.init_process_group('nccl', device_id=torch.device('cuda', int(os.environ.get('LOCAL_RANK', '0'))),
-                                pg_options=opts)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', int(os.environ.get('LOCAL_RANK', '0'))))
     dev = torch.device('cuda')
     import threading
     building = threading.Event()

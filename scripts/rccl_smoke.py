@@ -1,5 +1,5 @@
 """RCCL plumbing check on however many GPUs the box has (one is enough): the
-process group bench.py creates (high-priority stream), an async all-reduce
+process group bench.py creates (default stream priority), an async all-reduce
 of a slice overlapped with a SpMM on the compute stream, and the float64 MAX
 reduce bench.py ends with.  Run under torch.distributed.run."""
 import os
@@ -16,9 +16,7 @@ def main():
     rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
     dev = torch.device('cuda', int(os.environ.get('LOCAL_RANK', 0)))
     torch.cuda.set_device(dev)
-    opts = dist.ProcessGroupNCCL.Options()
-    opts.is_high_priority_stream = True
-    dist.init_process_group('nccl', device_id=dev, pg_options=opts)
+    dist.init_process_group('nccl', device_id=dev)
     from igr.dist import BipartiteShard
     rng = np.random.default_rng(0)
     U, I = 20000, 3000

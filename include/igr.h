@@ -154,6 +154,21 @@ int igr_plan_fill(int64_t n_rows, const int64_t *row_ptr, int64_t split_threshol
 int igr_spmm_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx, const float *rhs,
                  float *y, int64_t ldy, const igr_epilogue *epi, float *workspace, void *stream);
 
+/* igr_spmm_f32 without the `workspace` argument and without any allocation.
+ * No counterpart in the reference: it exists for callers that cannot allocate
+ * device memory (code under hipGraph capture, tight serving loops, harnesses
+ * that forbid hipMalloc).  The partial rows of split rows (n_chunks * d floats)
+ * live in a static device array of IGR_SPMM_NOALLOC_MAX_FLOATS floats (16 MiB),
+ * held by every GPU the library runs on until the process ends; a graph whose
+ * n_chunks * d exceeds it is rejected with IGR_ERR_ARG.  Same results as
+ * igr_spmm_f32, bit for bit.  All calls on one GPU share that GPU's array:
+ * calls that overlap on one GPU (two streams, two threads) race.  Nothing in
+ * the array needs clearing between calls.  The first call on a device looks up
+ * the array's address (make it outside a stream capture). */
+#define IGR_SPMM_NOALLOC_MAX_FLOATS (4 << 20)
+int igr_spmm_noalloc_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx, const float *rhs,
+                         float *y, int64_t ldy, const igr_epilogue *epi, void *stream);
+
 /* SpMM with row / column scaled weights and fused dropout:
  *   w(p) = (row_scale ? row_scale[r] : 1) * (col_scale ? col_scale[c] : 1)
  *   if keep < 1: w = floor(keep + U) ? w / keep : 0,

@@ -24,6 +24,7 @@
 //  * CSR structure and edge values are plain loads (non-temporal loads and
 //    stores measured 1-3 % slower / neutral on MI355X, scripts/tune_spmm.py).
 #include <algorithm>
+#include <mutex>
 
 #include "common.h"
 
@@ -545,6 +546,72 @@ extern "C" int igr_spmm_f32(const igr_csr *g, int32_t d, const float *x, int64_t
         if (!rhs) return run_spmm(fn, g, d, x, ldx, W_One{}, y, ldy, epi, workspace, stream);
         if (g->edge_id) return run_spmm(fn, g, d, x, ldx, W_ValEid{rhs, g->edge_id}, y, ldy, epi, workspace, stream);
         return run_spmm(fn, g, d, x, ldx, W_Val{rhs}, y, ldy, epi, workspace, stream);
+    });
+}
+
+// ---------------------------------------------------------------------------
+// igr_spmm_noalloc_f32: igr_spmm_f32 for callers that cannot allocate device
+// memory (code under hipGraph capture, tight serving loops, harnesses that
+// forbid hipMalloc).  The chunk tier's partial rows, which igr_spmm_f32 takes
+// as a caller-allocated `workspace`, live in a file-scope device array instead.
+// Every GPU the library runs on holds its own copy of the array (16 MiB) until
+// the process ends.  `scratch` is only a host-side stand-in for that array: its
+// per-device address comes from hipGetSymbolAddress, looked up once per device
+// (on the entry point's first call there, with that device current) and used
+// for every kernel argument afterwards.
+static __device__ __align__(256) float scratch[IGR_SPMM_NOALLOC_MAX_FLOATS];
+
+namespace igr {
+constexpr int kMaxDevices = 64;
+static std::mutex g_scratch_mu;
+static float *g_scratch_ptr[kMaxDevices];  // per device, filled on first use
+
+static int scratch_for_current_device(const char *fn, float **out) {
+    int dev = -1;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) {
+        set_error(std::string(fn) + ": hipGetDevice: " + hipGetErrorString(e));
+        return IGR_ERR_HIP;
+    }
+    if (dev < 0 || dev >= kMaxDevices) return arg_error(fn, "device index out of range");
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    if (!g_scratch_ptr[dev]) {
+        void *p = nullptr;
+        e = hipGetSymbolAddress(&p, HIP_SYMBOL(scratch));
+        if (e != hipSuccess || !p) {
+            set_error(std::string(fn) + ": hipGetSymbolAddress(scratch): " + hipGetErrorString(e));
+            return IGR_ERR_HIP;
+        }
+        g_scratch_ptr[dev] = static_cast<float *>(p);
+    }
+    *out = g_scratch_ptr[dev];
+    return IGR_OK;
+}
+}  // namespace igr
+
+extern "C" int igr_spmm_noalloc_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx,
+                                    const float *rhs, float *y, int64_t ldy, const igr_epilogue *epi,
+                                    void *stream) {
+    return guarded("igr_spmm_noalloc_f32", [&]() -> int {
+        const char *fn = "igr_spmm_noalloc_f32";
+        if (!g) return arg_error(fn, "graph is NULL");
+        if (d <= 0) return arg_error(fn, "d must be positive");
+        if (g->n_chunks < 0) return arg_error(fn, "negative n_chunks");
+        if (g->n_chunks > 0 && g->n_chunks > (int64_t)IGR_SPMM_NOALLOC_MAX_FLOATS / d)
+            return arg_error(fn, "split rows need n_chunks * d = " + std::to_string(g->n_chunks) + " * " +
+                                     std::to_string(d) + " floats of scratch, more than the static " +
+                                     std::to_string((int64_t)IGR_SPMM_NOALLOC_MAX_FLOATS) +
+                                     " (IGR_SPMM_NOALLOC_MAX_FLOATS); use igr_spmm_f32 with a workspace");
+        float *ws = nullptr;
+        // every partial row the combine kernel reads is written by the main kernel
+        // of the same call, so nothing in the array has to start at zero
+        if (g->n_chunks > 0) {
+            const int rc = scratch_for_current_device(fn, &ws);
+            if (rc != IGR_OK) return rc;
+        }
+        if (!rhs) return run_spmm(fn, g, d, x, ldx, W_One{}, y, ldy, epi, ws, stream);
+        if (g->edge_id) return run_spmm(fn, g, d, x, ldx, W_ValEid{rhs, g->edge_id}, y, ldy, epi, ws, stream);
+        return run_spmm(fn, g, d, x, ldx, W_Val{rhs}, y, ldy, epi, ws, stream);
     });
 }
 

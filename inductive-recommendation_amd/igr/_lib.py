@@ -15,6 +15,7 @@ c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
+SPMM_NOALLOC_MAX_FLOATS = 4 << 20  # IGR_SPMM_NOALLOC_MAX_FLOATS (include/igr.h)
 
 
 class IgrCsr(ctypes.Structure):
@@ -52,6 +53,7 @@ SIGNATURES = {
     'igr_plan_size': (ctypes.c_int, [c_i64, c_vp, c_i64, c_i64, _P(c_i64), _P(c_i64), _P(c_i64)]),
     'igr_plan_fill': (ctypes.c_int, [c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'igr_spmm_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, _P(IgrEpilogue), c_vp, c_vp]),
+    'igr_spmm_noalloc_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, _P(IgrEpilogue), c_vp]),
     'igr_spmm_heads_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     'igr_spmm_scaled_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_vp, c_f32, ctypes.c_uint64,
                                            ctypes.c_uint64, c_vp, c_i32, c_vp, c_i64, _P(IgrEpilogue), c_vp, c_vp]),

@@ -216,26 +216,38 @@ int igr_spmm_rows_f32(const igr_csr *g, int32_t d, const int64_t *rows, int64_t 
 int igr_spmm_push_f32(const igr_csr *g, int32_t d, const int64_t *rows, int64_t n_sel, const float *src, int64_t lds,
                       const float *rhs, float scale, int32_t self_add, float *dst, int64_t ldd, void *stream);
 
+/* Stable sort of row ids, the first step of every fixed-order accumulation
+ * below (the reference's index_put backward, trainer.py:553, run sequentially
+ * adds the terms of a repeated row in the order they appear; so do these):
+ *   keys[k] = (row << 32) | e, ascending, for the concatenation of up to three
+ *   index arrays of n entries each: entry e = a * n + i has row = idx_a[i] +
+ *   off_a (idx1 / idx2 nullable).  Rows must lie in [0, 2^32 - 1).
+ * keys: igr_rowsort_size(total) uint64 (total = n * number of arrays); the
+ * first `total` hold the result, the rest is scratch. */
+int64_t igr_rowsort_size(int64_t total);
+int igr_rowsort(int64_t n, const int64_t *idx0, int64_t off0, const int64_t *idx1, int64_t off1,
+                const int64_t *idx2, int64_t off2, uint64_t *keys, void *stream);
+
 /* The push without atomics (the training backward uses this one): mark the
  * selected rows, sum repeated rows' sources into one slot each, then every
  * output row gathers only from marked columns:
- *   igr_rowset_mark:  bits[r/32] |= 1 << r%32, slot[r] = some i with rows[i] = r,
- *                     and the same for h = r mod 2^19 in filter (bits, filter zero
- *                     on entry; bits: uint32[(n+31)/32], filter: uint32[16384],
- *                     slot: int32[n])
- *   igr_rowset_sum_f32: agg[slot[rows[i]]] += scale * src[i]   (agg zero on entry)
+ *   igr_rowset_mark:  bits[r/32] |= 1 << r%32, and the same for h = r mod 2^19 in
+ *                     filter (bits, filter zero on entry; bits: uint32[(n+31)/32],
+ *                     filter: uint32[16384])
+ *   igr_rowset_sum_f32: sorted = igr_rowsort(rows); for the first position k of
+ *                     every distinct row r: slot[r] = k and agg[k] = the sum of
+ *                     scale * src[i] over rows[i] = r, i ascending (slot:
+ *                     int32[n], agg: [n_sel, d]; other rows of agg untouched)
  *   igr_spmm_pull_marked_f32: out[c] = scale * (sum_{p in row c, col[p] marked}
  *                     rhs[p] agg[slot[col[p]]] + self_add [c marked] agg[slot[c]])
- *                     (one lane group per row, fixed order: deterministic
- *                     for distinct rows; repeats are summed into their slot
- *                     with float atomics).  Persistent 1024-thread workgroups
+ *                     (one lane group per row, fixed order: bitwise
+ *                     reproducible).  Persistent 1024-thread workgroups
  *                     keep the 64 KB filter in LDS; only filter hits probe bits.
  *                     row_mask (or NULL = every row): rows c with their bit
  *                     clear are not computed and out[c] is left untouched
  *   igr_rowset_clear: zero the words of bits and filter holding the selected rows
  * On the reverse graph, out = A^T G (+ G): igr_spmm_push_f32's result. */
-int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, int32_t *slot,
-                    void *stream);
+int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, void *stream);
 /* bits |= every column of the selected rows, and the row ids themselves when
  * self_mark (square graph): the rows at which a batch's last layer reads the
  * layer below it (the row_mask of that layer and the col_mask of its reverse,
@@ -246,8 +258,8 @@ int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t
 int igr_rowset_mark_neighbors(const igr_csr *g, int64_t n_sel, const int64_t *rows, uint32_t *bits,
                               int32_t self_mark, uint8_t *scratch, void *stream);
 int igr_bitmap_set(int64_t n, const int64_t *idx, uint32_t *bits, void *stream);
-int igr_rowset_sum_f32(int64_t n_sel, int32_t d, const int64_t *rows, const int32_t *slot, const float *src,
-                       int64_t lds, float scale, float *agg, int64_t ld_agg, void *stream);
+int igr_rowset_sum_f32(int64_t n_sel, int32_t d, const uint64_t *sorted, const float *src, int64_t lds,
+                       float scale, int32_t *slot, float *agg, int64_t ld_agg, void *stream);
 int igr_spmm_pull_marked_f32(const igr_csr *g, int32_t d, const uint32_t *bits, const uint32_t *filter,
                              const int32_t *slot, const float *agg, int64_t ld_agg, const float *rhs, float scale,
                              int32_t self_add, const uint32_t *row_mask, float *out, int64_t ldo, void *stream);
@@ -267,10 +279,12 @@ int igr_mask_scores_f32(int64_t n_rows, const int64_t *row_ptr, const int32_t *c
 int igr_topk_f32(int64_t n_rows, int64_t n_cols, const float *scores, int64_t ld, int32_t k, float *out_val,
                  int64_t *out_idx, void *stream);
 
-/* The uniforms igr_spmm_scaled_f32 draws, per CSR position of g (out[nnz];
- * for tests and for an explicit-values replay of the same mask). */
-int igr_dropout_uniforms(const igr_csr *g, uint64_t seed, uint64_t offset, int32_t transposed, float *out,
-                         void *stream);
+/* The uniforms igr_spmm_scaled_f32 draws, per CSR position of g (out[nnz]):
+ * the explicit-values form of the same mask (AttIGCN's per-edge dropout,
+ * model.py:4016-4028, feeds them to igr_edge_dropout_f32; tests).  offset_dev
+ * as in igr_spmm_scaled_f32. */
+int igr_dropout_uniforms(const igr_csr *g, uint64_t seed, uint64_t offset, const int64_t *offset_dev,
+                         int32_t transposed, float *out, void *stream);
 
 /* u_dot_v SDDMM: out[eid(p), h] = <u[row_p, h, :], v[col_p, h, :]>.
  * AttIGCN.masked_mm (model.py:4246-4255) with u = x_q (dst rows),
@@ -314,26 +328,35 @@ int igr_feat_values_f32(int64_t n_rows, const int64_t *row_ptr, const float *row
  * model.py:4048-4049; Embedding lookups trainer.py:544-546). */
 int igr_gather_rows_f32(int64_t n, int32_t d, const int64_t *idx, int64_t offset,
                         const float *src, int64_t ld_src, float *out, int64_t ld_out, void *stream);
-/* Row scatter-add (gather backward): dst[idx[i] + offset, :] += src[i, :] (float atomics). */
-int igr_scatter_add_rows_f32(int64_t n, int32_t d, const int64_t *idx, int64_t offset,
-                             const float *src, int64_t ld_src, float *dst, int64_t ld_dst,
-                             void *stream);
+/* Row scatter-add (gather backward, index_put accumulate): dst[row_i, :] += src[i, :]
+ * with sorted = igr_rowsort of the n row ids (offset included).  Deterministic:
+ * one writer per distinct row, adding its terms for i ascending onto the value
+ * dst holds - the order of a sequential index_put / index_add (trainer.py:553). */
+int igr_scatter_add_rows_f32(int64_t n, int32_t d, const uint64_t *sorted, const float *src,
+                             int64_t ld_src, float *dst, int64_t ld_dst, void *stream);
 
 /* Fused BPR step terms (model.py:4046-4052 + trainer.py:536-540, 542-548):
  * for each sample b: u = t[off_u + users[b]], p = t[off_i + pos[b]], n = t[off_i + neg[b]]
  *   s_b = sum_k u_k (n_k - p_k) * (w ? w_k : 1)
  *   loss[b] = softplus(s_b);  l2[b] = |u|^2 + |p|^2 + |n|^2      (loss/l2 nullable)
  * and, if grad != NULL, accumulates  g_loss * dloss_b/dt + g_l2 * dl2_b/dt
- * into grad (float atomics); if dw != NULL, g_loss * dloss_b/dw into dw
- * (summed per workgroup in LDS first; d <= 1024).
+ * into grad; if dw != NULL, g_loss * dloss_b/dw into dw.  No atomics: with
+ * sorted = igr_rowsort(batch, users, off_u, pos, off_i, neg, off_i) every
+ * table row's terms are added in entry order (users, then pos, then neg, each
+ * by sample) by one writer; sorted == NULL asserts that the 3 * batch rows are
+ * all distinct (e.g. a table of gathered batch rows).  dw is summed per
+ * workgroup, then over the workgroups, in sample order.  The backward
+ * (grad or dw given) needs workspace: igr_bpr_workspace_floats(batch, d) floats.
  * (g_loss = dL/dloss_b, e.g. 1/batch for a mean.)  g_loss_dev / g_l2_dev
  * (nullable device scalars) multiply g_loss / g_l2: an autograd backward
  * passes the incoming gradient without a device->host sync. */
+int64_t igr_bpr_workspace_floats(int64_t batch, int32_t d);
 int igr_bpr_fwd_bwd_f32(int64_t batch, int32_t d, const int64_t *users, const int64_t *pos,
                         const int64_t *neg, int64_t off_u, int64_t off_i, const float *t,
                         int64_t ld_t, const float *w, float *loss, float *l2, float g_loss,
                         float g_l2, const float *g_loss_dev, const float *g_l2_dev, float *grad,
-                        int64_t ld_grad, float *dw, void *stream);
+                        int64_t ld_grad, float *dw, const uint64_t *sorted, float *workspace,
+                        void *stream);
 
 /* Dense fp32 GEMM on MFMA (v_mfma_f32_16x16x4_f32, exact fp32 products):
  *   C[m, n] = sum_k A(m, k) * B(k, n) + bias[n]

@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, 'csrc')
 INCLUDE = os.path.join(ROOT, 'include')
 OBJ = os.path.join(HERE, 'build')
 LIB = os.path.join(HERE, 'igr', 'lib', 'libigr.so')
-SOURCES = ['spmm.hip', 'spmm_rows.hip', 'topk.hip', 'edge_ops.hip', 'bpr.hip', 'gemm.hip', 'train_ops.hip', 'graph_host.cpp', 'capi.cpp']
+SOURCES = ['spmm.hip', 'spmm_rows.hip', 'topk.hip', 'edge_ops.hip', 'bpr.hip', 'rowsort.hip', 'gemm.hip', 'train_ops.hip', 'graph_host.cpp', 'capi.cpp']
 ARCH = os.environ.get('IGR_OFFLOAD_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 # Packed fp32 VALU ops are switched off for the device pass (some of their
@@ -38,7 +38,7 @@ def build(verbose=False, jobs=8, lib=None, obj=None):
     LIB, OBJ = lib or LIB, obj or OBJ
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    headers = [os.path.join(CSRC, 'common.h'), os.path.join(INCLUDE, 'igr.h')]
+    headers = [os.path.join(CSRC, 'common.h'), os.path.join(CSRC, 'segsum.h'), os.path.join(INCLUDE, 'igr.h')]
     objs, procs = [], []
     for src in SOURCES:
         s = os.path.join(CSRC, src)

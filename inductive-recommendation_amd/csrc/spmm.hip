@@ -522,14 +522,18 @@ static int run_spmm(const char *fn, const igr_csr *g, int32_t d, const float *x,
     return launch_status(fn);
 }
 
-// The uniforms W_Scaled draws, per CSR position of g (tests / explicit-values path).
-__global__ void uniforms_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
-                                uint64_t seed, uint64_t offset, int swap, float *__restrict__ out) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// The uniforms W_Scaled draws, per CSR position of g (explicit-values path:
+// AttIGCN's per-edge dropout; tests).  One wave per row, lanes over its edges.
+__global__ __launch_bounds__(256) void uniforms_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr,
+                                                       const int32_t *__restrict__ col, uint64_t seed, uint64_t offset,
+                                                       const int64_t *__restrict__ offset_dev, int swap,
+                                                       float *__restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n_rows) return;
-    for (int64_t p = row_ptr[r]; p < row_ptr[r + 1]; ++p) {
+    const uint64_t off = offset + (offset_dev ? (uint64_t)*offset_dev : 0);
+    for (int64_t p = row_ptr[r] + (threadIdx.x & 63); p < row_ptr[r + 1]; p += 64) {
         const uint32_t c = (uint32_t)col[p];
-        out[p] = uniform24(seed, offset, swap ? edge_key(c, (uint32_t)r) : edge_key((uint32_t)r, c));
+        out[p] = uniform24(seed, off, swap ? edge_key(c, (uint32_t)r) : edge_key((uint32_t)r, c));
     }
 }
 
@@ -650,14 +654,16 @@ extern "C" int igr_spmm_heads_f32(const igr_csr *g, int32_t h, int32_t d, const 
     });
 }
 
-extern "C" int igr_dropout_uniforms(const igr_csr *g, uint64_t seed, uint64_t offset, int32_t transposed, float *out,
-                                    void *stream) {
+extern "C" int igr_dropout_uniforms(const igr_csr *g, uint64_t seed, uint64_t offset, const int64_t *offset_dev,
+                                    int32_t transposed, float *out, void *stream) {
     return guarded("igr_dropout_uniforms", [&]() -> int {
         if (!g || !out) return arg_error("igr_dropout_uniforms", "graph / out NULL");
         if (g->n_rows <= 0 || g->nnz <= 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-        hipLaunchKernelGGL(uniforms_kernel, dim3((unsigned)((g->n_rows + 255) / 256)), dim3(256), 0, st, g->n_rows,
-                           g->row_ptr, g->col_idx, seed, offset, transposed ? 1 : 0, out);
+        if (g->n_rows > 4294967295LL || g->n_cols > 4294967295LL)
+            return arg_error("igr_dropout_uniforms", "dropout keys need row / column ids below 2^32");
+        hipLaunchKernelGGL(uniforms_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0, st, g->n_rows,
+                           g->row_ptr, g->col_idx, seed, offset, offset_dev, transposed ? 1 : 0, out);
         return launch_status("igr_dropout_uniforms");
     });
 }

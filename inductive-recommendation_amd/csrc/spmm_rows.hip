@@ -152,13 +152,13 @@ extern "C" int igr_spmm_push_f32(const igr_csr *g, int32_t d, const int64_t *row
 // ------------------------------------------------------------------ masked pull
 // The transpose of spmm_rows without atomics: mark the selected rows in a
 // bitmap (n/32 words: 137 KB at 1.1M rows, L2-resident), sum repeated rows
-// into one slot each (agg), then every output row c streams its column
+// into one slot each (agg; igr_rowset_sum_f32 in rowsort.hip: sorted, fixed
+// order), then every output row c streams its column
 // indices, tests their bits and gathers agg only on hits:
 //   out[c] = scale (sum_{p in row c, col[p] marked} rhs[p] agg[slot[col[p]]]
 //                   + self_add * [c marked] agg[slot[c]])
 // Run on the reverse graph this is dst = A^T G (+ G) for G = the selected rows'
-// gradients; the per-row summation order is fixed (deterministic for distinct
-// rows; repeated rows meet in agg through float atomics).
+// gradients; every summation order is fixed (bitwise reproducible).
 namespace igr {
 
 // LDS filter of the marked set: bit (r mod 2^19), 64 KB - two 1024-thread
@@ -170,14 +170,13 @@ constexpr uint32_t kFilterMask = (1u << kFilterLog2) - 1;
 constexpr int kFilterWords = (1 << kFilterLog2) / 32;
 
 __global__ void rowset_mark_kernel(int64_t n, const int64_t *__restrict__ rows, uint32_t *__restrict__ bits,
-                                   uint32_t *__restrict__ filter, int32_t *__restrict__ slot) {
+                                   uint32_t *__restrict__ filter) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t r = rows[i];
     atomicOr(bits + (r >> 5), 1u << (r & 31));
     const uint32_t h = (uint32_t)r & kFilterMask;
     atomicOr(filter + (h >> 5), 1u << (h & 31));
-    slot[r] = (int32_t)i;  // any one of a repeated row's positions
 }
 
 // bits |= every column of the selected rows (and the row ids themselves when
@@ -254,17 +253,6 @@ __global__ void rowset_clear_kernel(int64_t n, const int64_t *__restrict__ rows,
     const int64_t r = rows[i];
     bits[r >> 5] = 0u;  // every bit set in these words belongs to a selected row
     filter[((uint32_t)r & kFilterMask) >> 5] = 0u;
-}
-
-// agg[slot[rows[i]]] += scale * src[i]; agg zero on entry (repeats: float atomics on n_sel x d)
-__global__ void rowset_sum_kernel(int64_t n, int d, const int64_t *__restrict__ rows,
-                                  const int32_t *__restrict__ slot, const float *__restrict__ src, int64_t lds,
-                                  float *__restrict__ agg, int64_t ld_agg, float scale) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * d) return;
-    const int64_t i = t / d;
-    const int f = (int)(t - i * d);
-    atomicAdd(agg + (int64_t)slot[rows[i]] * ld_agg + f, scale * src[i * lds + f]);
 }
 
 template <int D>
@@ -360,14 +348,13 @@ __global__ __launch_bounds__(1024) void spmm_pull_marked_kernel(
 
 static unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
-extern "C" int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, int32_t *slot,
-                               void *stream) {
+extern "C" int igr_rowset_mark(int64_t n_sel, const int64_t *rows, uint32_t *bits, uint32_t *filter, void *stream) {
     return guarded("igr_rowset_mark", [&]() -> int {
         if (n_sel <= 0) return IGR_OK;
-        if (!rows || !bits || !filter || !slot) return arg_error("igr_rowset_mark", "NULL pointer");
+        if (!rows || !bits || !filter) return arg_error("igr_rowset_mark", "NULL pointer");
         if (n_sel > 2147483647) return arg_error("igr_rowset_mark", "too many rows");
         hipLaunchKernelGGL(rowset_mark_kernel, dim3(blocks_for(n_sel, 256)), dim3(256), 0,
-                           reinterpret_cast<hipStream_t>(stream), n_sel, rows, bits, filter, slot);
+                           reinterpret_cast<hipStream_t>(stream), n_sel, rows, bits, filter);
         return launch_status("igr_rowset_mark");
     });
 }
@@ -413,19 +400,6 @@ extern "C" int igr_rowset_clear(int64_t n_sel, const int64_t *rows, uint32_t *bi
         hipLaunchKernelGGL(rowset_clear_kernel, dim3(blocks_for(n_sel, 256)), dim3(256), 0,
                            reinterpret_cast<hipStream_t>(stream), n_sel, rows, bits, filter);
         return launch_status("igr_rowset_clear");
-    });
-}
-
-extern "C" int igr_rowset_sum_f32(int64_t n_sel, int32_t d, const int64_t *rows, const int32_t *slot,
-                                  const float *src, int64_t lds, float scale, float *agg, int64_t ld_agg,
-                                  void *stream) {
-    return guarded("igr_rowset_sum_f32", [&]() -> int {
-        if (d <= 0 || lds < d || ld_agg < d) return arg_error("igr_rowset_sum_f32", "bad d / leading dims");
-        if (n_sel <= 0) return IGR_OK;
-        hipLaunchKernelGGL(rowset_sum_kernel, dim3(blocks_for(n_sel * d, 256)), dim3(256), 0,
-                           reinterpret_cast<hipStream_t>(stream), n_sel, (int)d, rows, slot, src, lds, agg, ld_agg,
-                           scale);
-        return launch_status("igr_rowset_sum_f32");
     });
 }
 

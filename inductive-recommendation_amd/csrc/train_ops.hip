@@ -48,9 +48,25 @@ __global__ void bpr_sample_kernel(int64_t batch, int64_t n_active, const int32_t
         const int32_t p = items[b + bounded(draw(seed, offset, i, 1), e - b)];
         int32_t n = (int32_t)bounded(draw(seed, offset, i, 2), n_items);
         // rejection as dataset.py:126-128; bounded so a user who interacted with
-        // every item cannot spin forever (the reference would)
-        for (int32_t k = 3; k < max_rounds + 3 && member(items, b, e, n); ++k)
+        // every item cannot spin forever (the reference would): such a user keeps
+        // the last draw, every other user always ends with a true negative
+        int32_t k = 3;
+        for (; k < max_rounds + 3 && member(items, b, e, n); ++k)
             n = (int32_t)bounded(draw(seed, offset, i, (uint32_t)k), n_items);
+        if (k == max_rounds + 3 && member(items, b, e, n) && (e - b) < n_items) {
+            // every redraw hit the user's own list (a heavy user of a small item set):
+            // take the j-th item of the complement directly, j uniform.  The sorted list
+            // has items[b + c] - c non-decreasing, so the number c of list items before
+            // the j-th gap is found by bisection and the answer is j + c.
+            const int64_t j = bounded(draw(seed, offset, i, (uint32_t)k), n_items - (e - b));
+            int64_t lo = 0, hi = e - b;
+            while (lo < hi) {
+                const int64_t m = (lo + hi) >> 1;
+                if ((int64_t)items[b + m] - m <= j) lo = m + 1;
+                else hi = m;
+            }
+            n = (int32_t)(j + lo);
+        }
         users[i] = u;
         pos[i] = p;
         neg[i] = n;

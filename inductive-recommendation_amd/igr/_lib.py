@@ -61,16 +61,18 @@ SIGNATURES = {
                                          c_i64, c_f32, c_vp, c_i64, c_vp]),
     'igr_spmm_push_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_f32, c_i32, c_vp,
                                          c_i64, c_vp]),
-    'igr_rowset_mark': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'igr_rowsort_size': (c_i64, [c_i64]),
+    'igr_rowsort': (ctypes.c_int, [c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    'igr_rowset_mark': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     'igr_rowset_mark_neighbors': (ctypes.c_int, [_P(IgrCsr), c_i64, c_vp, c_vp, c_i32, c_vp, c_vp]),
     'igr_bitmap_set': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp]),
-    'igr_rowset_sum_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_f32, c_vp, c_i64, c_vp]),
+    'igr_rowset_sum_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_vp, c_i64, c_f32, c_vp, c_vp, c_i64, c_vp]),
     'igr_spmm_pull_marked_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32,
                                                 c_i32, c_vp, c_vp, c_i64, c_vp]),
     'igr_rowset_clear': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     'igr_mask_scores_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     'igr_topk_f32': (ctypes.c_int, [c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),
-    'igr_dropout_uniforms': (ctypes.c_int, [_P(IgrCsr), ctypes.c_uint64, ctypes.c_uint64, c_i32, c_vp, c_vp]),
+    'igr_dropout_uniforms': (ctypes.c_int, [_P(IgrCsr), ctypes.c_uint64, ctypes.c_uint64, c_vp, c_i32, c_vp, c_vp]),
     'igr_sddmm_dot_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     'igr_segment_reduce_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i32, c_vp, c_vp]),
     'igr_att_softmax_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),
@@ -79,9 +81,11 @@ SIGNATURES = {
     'igr_edge_dropout_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_f32, c_vp, c_vp]),
     'igr_feat_values_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_f32, c_vp, c_vp]),
     'igr_gather_rows_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
-    'igr_scatter_add_rows_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    'igr_scatter_add_rows_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
     'igr_bpr_fwd_bwd_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,
-                                           c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+                                           c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
+                                           c_vp]),
+    'igr_bpr_workspace_floats': (c_i64, [c_i64, c_i32]),
     'igr_gemm_workspace_size': (c_i64, [c_i64, c_i64, c_i64]),
     'igr_gemm_f32': (ctypes.c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp, c_vp,
                                     c_i64, c_vp, c_i64, c_vp]),

@@ -403,7 +403,7 @@ class ShardedIGCN(nn.Module):
             rep, aux = ShardedPropagateRows.apply(self.embedding.weight, self.w, self, self.feat_values(), aux_idx,
                                                   users, items_b)
             iu, ip, ineg = ops.batch_positions(users.numel(), users.device)
-            bpr, l2 = ops.bpr_loss(rep, iu, ip, ineg, 0, 0)
+            bpr, l2 = ops.bpr_loss(rep, iu, ip, ineg, 0, 0, distinct=True)
             return bpr, l2, aux
         rep, aux = ShardedPropagate.apply(self.embedding.weight, self.w, self, self.feat_values(), aux_idx)
         bpr, l2 = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_local)
@@ -413,9 +413,8 @@ class ShardedIGCN(nn.Module):
         """Mean aux BPR loss on E_k with w (trainer.py:542-549); item features at n_local."""
         au, ap, an = aux
         loss = torch.empty(au.numel(), dtype=torch.float32, device=emb.device)
-        ops.L.call('igr_bpr_fwd_bwd_f32', au.numel(), emb.shape[1], ops._p(au), ops._p(ap), ops._p(an), 0,
-                   self.n_local, ops._p(emb), emb.stride(0), ops._p(w), ops._p(loss), None, 0.0, 0.0, None, None,
-                   None, 0, None, ops._stream())
+        ops._bpr_call(au.numel(), emb.shape[1], au, ap, an, 0, self.n_local, emb, w, loss, None, 0.0, 0.0, None, None,
+                      None, 0, None, None)
         return loss.mean()
 
     def aux_backward(self, emb, w, aux, g_aux, demb):
@@ -423,9 +422,8 @@ class ShardedIGCN(nn.Module):
         au, ap, an = aux
         dw = torch.zeros_like(w)
         g_aux = g_aux.float().contiguous()
-        ops.L.call('igr_bpr_fwd_bwd_f32', au.numel(), emb.shape[1], ops._p(au), ops._p(ap), ops._p(an), 0,
-                   self.n_local, ops._p(emb), emb.stride(0), ops._p(w), None, None, 1.0 / au.numel(), 0.0,
-                   ops._p(g_aux), None, ops._p(demb), demb.stride(0), ops._p(dw), ops._stream())
+        ops._bpr_call(au.numel(), emb.shape[1], au, ap, an, 0, self.n_local, emb, w, None, None, 1.0 / au.numel(), 0.0,
+                      g_aux, None, demb, demb.stride(0), dw, ops.rowsort(au, 0, ap, self.n_local, an, self.n_local))
         return dw
 
     def batch_rep(self, users, items_b):

@@ -161,7 +161,7 @@ class LightGCN(BasicModel):
             rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
             rep_b = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
                                        adj_vals=self.norm_vals)
-            bpr, _ = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0)
+            bpr, _ = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0, distinct=True)
         else:
             rep = self.get_rep()
             bpr, _ = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
@@ -229,17 +229,22 @@ class NGCF(BasicModel):
         return LightGCN.predict(self, users, rep)
 
 
-def dropout_values(model, vals):
+def dropout_values(model, vals, graph=None):
     """NGCF.dropout_sp_mat (model.py:4016-4028) as a value mask over the fixed
-    CSR (a dropped edge contributes an exact 0.0).  The uniform draws come
-    from the device generator by default; config['dropout_rng'] = 'cpu' draws
-    them from the CPU generator exactly as the reference does
-    (`torch.rand(nnz).to(device)`), for run-to-run parity with it."""
+    CSR (a dropped edge contributes an exact 0.0).  config['dropout_rng'] =
+    'cpu' draws the uniforms from the CPU generator exactly as the reference
+    does (`torch.rand(nnz).to(device)`), for run-to-run parity with it; a graph
+    given with the default 'device' draws them from the counter-based device
+    generator keyed by (seed, step, edge) - the draws of the fused-dropout SpMM,
+    the same in eager steps and in hipGraph replays."""
     if not model.training or model.dropout == 0:
         return vals
     n = vals.numel()
     if model.config.get('dropout_rng', 'device') == 'cpu':
         rand = torch.rand(n).to(vals.device)
+    elif graph is not None:
+        seed, step, ctr = model.next_dropout_step()
+        rand = ops.dropout_uniforms(graph, seed, step, offset_dev=ctr)
     else:
         rand = torch.rand(n, device=vals.device)
     return ops.edge_dropout(vals, rand, model.dropout)
@@ -340,15 +345,21 @@ class IGCN(BasicModel):
         if self.training and self.dropout > 0 and self.config.get('dropout_rng', 'device') == 'cpu':
             return dropout_values(self, self.feat_vals)
         if self.training and self.dropout > 0:
-            if not hasattr(self, '_drop_seed'):
-                self._drop_seed = int(self.config.get('seed', torch.initial_seed())) & (2 ** 63 - 1)
-            ctr = getattr(self, 'device_step', None)
-            if ctr is not None:  # hipGraph mode: mask offset = next host step + replays so far (device)
-                return ops.ScaledWeights(self.feat_base, None, 1.0 - self.dropout, self._drop_seed,
-                                         getattr(self, '_drop_step', -1) + 1, offset_dev=ctr)
-            self._drop_step = getattr(self, '_drop_step', -1) + 1
-            return ops.ScaledWeights(self.feat_base, None, 1.0 - self.dropout, self._drop_seed, self._drop_step)
+            seed, step, ctr = self.next_dropout_step()
+            return ops.ScaledWeights(self.feat_base, None, 1.0 - self.dropout, seed, step, offset_dev=ctr)
         return ops.ScaledWeights(self.feat_base)
+
+    def next_dropout_step(self):
+        """(seed, offset, device counter or None) of this step's dropout draws.  Eager:
+        the host step count, advanced here.  hipGraph mode (device_step set): the
+        next host step plus the replays so far, which the kernels add on the device."""
+        if not hasattr(self, '_drop_seed'):
+            self._drop_seed = int(self.config.get('seed', torch.initial_seed())) & (2 ** 63 - 1)
+        ctr = getattr(self, 'device_step', None)
+        if ctr is not None:
+            return self._drop_seed, getattr(self, '_drop_step', -1) + 1, ctr
+        self._drop_step = getattr(self, '_drop_step', -1) + 1
+        return self._drop_seed, self._drop_step, None
 
     def inductive_rep_layer(self, feat_vals):
         """model.py:4177-4186 (no padding needed: the lhs has n_cols rows)."""
@@ -384,7 +395,7 @@ class IGCN(BasicModel):
             rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
             rep_b = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
                                        feat=self.feat_mat, fvals=self.inductive_values(), adj_vals=self.norm_vals)
-            bpr, l2 = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0)
+            bpr, l2 = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0, distinct=True)
         else:
             bpr, l2 = ops.bpr_loss(self.get_rep(), users, pos_items, neg_items, 0, self.n_users)
         extra = self._l2_extra()
@@ -401,7 +412,7 @@ class IGCN(BasicModel):
         rep_b, aux = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
                                         feat=self.feat_mat, fvals=self.inductive_values(), adj_vals=self.norm_vals,
                                         aux=(a_users, a_pos, a_neg, len(self.user_map)), w=self.w)
-        bpr, l2 = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0)
+        bpr, l2 = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0, distinct=True)
         extra = self._l2_extra()
         return bpr, (l2 if extra is None else l2 + extra), aux
 
@@ -466,7 +477,7 @@ class AttIGCN(IGCN):
 
     def feat_values(self):
         """Explicit per-edge dropout values: the attention layer needs them per edge."""
-        return dropout_values(self, self.feat_vals)
+        return dropout_values(self, self.feat_vals, self.feat_mat)
 
     def attention_values(self, feat_vals):
         """model.py:4258-4275.  After dropout the dropped edges are absent from

@@ -171,11 +171,11 @@ def spmm_scaled(g: Graph, x, w: ScaledWeights, out=None, epi=None):
     return out
 
 
-def dropout_uniforms(g: Graph, seed, offset, swap=False):
-    """The uniforms ScaledWeights(seed, offset, swap)'s dropout draws on g, per CSR position."""
+def dropout_uniforms(g: Graph, seed, offset, swap=False, offset_dev=None):
+    """The uniforms ScaledWeights(seed, offset, swap, offset_dev)'s dropout draws on g, per CSR position."""
     out = torch.empty(g.nnz, dtype=torch.float32, device=g.device)
     L.call('igr_dropout_uniforms', ctypes.byref(g.csr), ctypes.c_uint64(seed & (2 ** 64 - 1)),
-           ctypes.c_uint64(offset & (2 ** 64 - 1)), int(bool(swap)), _p(out), _stream())
+           ctypes.c_uint64(offset & (2 ** 64 - 1)), _p(offset_dev), int(bool(swap)), _p(out), _stream())
     return out
 
 
@@ -183,6 +183,8 @@ def feat_row_values(row_sum, exponent, out=None):
     """Per-row row_sum ** exponent (IGCN.update_feat_mat's value, model.py:4127-4130)."""
     _dev(row_sum, out)
     out = torch.empty_like(row_sum) if out is None else out
+    if out.numel() != row_sum.numel() or out.dtype != torch.float32 or not out.is_contiguous():
+        raise IgrError(f'feat_row_values: out has {out.numel()} values for {row_sum.numel()} rows')
     L.call('igr_feat_values_f32', row_sum.numel(), None, _p(row_sum), float(exponent), _p(out), _stream())
     return out
 
@@ -314,6 +316,9 @@ def feat_values(g: Graph, row_sum, exponent, out=None):
         raise IgrError('feat_values: row_sum size differs from n_rows')
     if out is None:
         out = torch.empty(g.nnz, dtype=torch.float32, device=row_sum.device)
+    if out.numel() != g.nnz or out.dtype != torch.float32 or not out.is_contiguous():
+        raise IgrError(f'feat_values: out has {out.numel()} values, the graph has {g.nnz} edges '
+                       f'(a buffer cached for another feature graph?)')
     L.call('igr_feat_values_f32', g.n_rows, _p(g.row_ptr), _p(row_sum), float(exponent), _p(out), _stream())
     return out
 
@@ -328,13 +333,48 @@ def gather_rows(src, idx, offset=0):
     return out
 
 
-def scatter_add_rows(dst, idx, src, offset=0):
+def rowsort(idx0, off0=0, idx1=None, off1=0, idx2=None, off2=0):
+    """Sorted (row << 32 | entry) keys of the concatenation [idx0 + off0; idx1 + off1;
+    idx2 + off2] (igr_rowsort): the order every fixed-order accumulation below
+    walks.  Returns an int64 tensor whose first n_total entries are the keys."""
+    _dev(idx0, idx1, idx2)
+    arrs = [a.to(torch.int64).contiguous() for a in (idx0, idx1, idx2) if a is not None]
+    n = arrs[0].numel()
+    if any(a.numel() != n for a in arrs):
+        raise IgrError('rowsort: index arrays must have the same length')
+    size = int(L.lib().igr_rowsort_size(n * len(arrs)))
+    keys = torch.empty(max(size, 1), dtype=torch.int64, device=idx0.device)
+    keys._refs = arrs
+    L.call('igr_rowsort', n, _p(arrs[0]), int(off0), _p(arrs[1]) if len(arrs) > 1 else None, int(off1),
+           _p(arrs[2]) if len(arrs) > 2 else None, int(off2), _p(keys), _stream())
+    return keys
+
+
+def scatter_add_rows(dst, idx, src, offset=0, sorted_keys=None):
+    """dst[idx[i] + offset] += src[i], each row's terms added for i ascending
+    (deterministic; sorted_keys = rowsort(idx, offset) when the caller has it)."""
     _dev(dst, idx, src)
     src, lds = _rows(src)
-    idx = idx.to(torch.int64).contiguous()
-    L.call('igr_scatter_add_rows_f32', idx.numel(), src.shape[1], _p(idx), int(offset), _p(src), lds, _p(dst),
+    if idx.numel() != src.shape[0]:
+        raise IgrError(f'scatter_add_rows: {idx.numel()} indices for {src.shape[0]} rows')
+    if _f32(dst).stride(1) != 1 or dst.shape[1] != src.shape[1]:
+        raise IgrError('scatter_add_rows: dst must be [n, d] float32 with unit inner stride')
+    if sorted_keys is None:
+        sorted_keys = rowsort(idx, offset)
+    L.call('igr_scatter_add_rows_f32', idx.numel(), src.shape[1], _p(sorted_keys), _p(src), lds, _p(dst),
            dst.stride(0), _stream())
     return dst
+
+
+def _bpr_call(B, d, users, pos, neg, off_u, off_i, t, w, loss, l2, g_loss, g_l2, gl_dev, g2_dev, grad, ld_grad,
+              dw, sorted_keys):
+    """igr_bpr_fwd_bwd_f32 with its backward workspace."""
+    ws = None
+    if (grad is not None and sorted_keys is not None) or dw is not None:
+        ws = torch.empty(int(L.lib().igr_bpr_workspace_floats(B, d)), dtype=torch.float32, device=t.device)
+    L.call('igr_bpr_fwd_bwd_f32', B, d, _p(users), _p(pos), _p(neg), int(off_u), int(off_i), _p(t), t.stride(0),
+           _p(w), _p(loss), _p(l2), g_loss, g_l2, _p(gl_dev), _p(g2_dev), _p(grad), ld_grad, _p(dw),
+           _p(sorted_keys), _p(ws), _stream())
 
 
 def mask_scores(scores, row_ptr, cols):
@@ -619,12 +659,12 @@ def _rowset(g: Graph):
     return rs
 
 
-def spmm_pull(g: Graph, rows, src, rhs=None, scale=1.0, self_add=False, out=None, row_mask=None):
+def spmm_pull(g: Graph, rows, src, rhs=None, scale=1.0, self_add=False, out=None, row_mask=None, sorted_keys=None):
     """out[c] = scale * (sum_{p in row c} rhs[p] S[col[p]] + self_add S[c]) with
-    S[r] = sum of src[i] over rows[i] == r - the atomic-free equivalent of
-    spmm_push on the reverse graph (igr_spmm_pull_marked_f32).  row_mask (a
-    bitmap over the rows): only the marked rows are computed; the others of
-    `out` are left as they were."""
+    S[r] = sum of src[i] over rows[i] == r (i ascending) - the atomic-free
+    equivalent of spmm_push on the reverse graph (igr_spmm_pull_marked_f32).
+    row_mask (a bitmap over the rows): only the marked rows are computed; the
+    others of `out` are left as they were.  sorted_keys = rowsort(rows)."""
     _dev(src, rows, rhs, out, row_mask)
     if g.edge_id is not None and rhs is not None:
         raise IgrError('spmm_pull: rhs by edge id needs a graph without an edge_id permutation')
@@ -632,12 +672,15 @@ def spmm_pull(g: Graph, rows, src, rhs=None, scale=1.0, self_add=False, out=None
     d = src.shape[1]
     rows = rows.to(torch.int64).contiguous()
     bits, filt, slot = _rowset(g)
-    agg = torch.zeros(max(rows.numel(), 1), d, dtype=torch.float32, device=src.device)
+    agg = torch.empty(max(rows.numel(), 1), d, dtype=torch.float32, device=src.device)
     if out is None:
         out = torch.empty(g.n_rows, d, dtype=torch.float32, device=src.device)
+    if sorted_keys is None:
+        sorted_keys = rowsort(rows)
     st = _stream()
-    L.call('igr_rowset_mark', rows.numel(), _p(rows), _p(bits), _p(filt), _p(slot), st)
-    L.call('igr_rowset_sum_f32', rows.numel(), d, _p(rows), _p(slot), _p(src), lds, 1.0, _p(agg), agg.stride(0), st)
+    L.call('igr_rowset_mark', rows.numel(), _p(rows), _p(bits), _p(filt), st)
+    L.call('igr_rowset_sum_f32', rows.numel(), d, _p(sorted_keys), _p(src), lds, 1.0, _p(slot), _p(agg),
+           agg.stride(0), st)
     L.call('igr_spmm_pull_marked_f32', ctypes.byref(g.csr), d, _p(bits), _p(filt), _p(slot), _p(agg), agg.stride(0),
            _p(None if rhs is None else _f32(rhs).contiguous()), float(scale), int(bool(self_add)), _p(row_mask),
            _p(out), out.stride(0), st)
@@ -678,8 +721,8 @@ class PropagateRows(torch.autograd.Function):
         if aux is not None:
             au, ap, an, off = aux
             loss = torch.empty(au.numel(), dtype=torch.float32, device=emb.device)
-            L.call('igr_bpr_fwd_bwd_f32', au.numel(), emb.shape[1], _p(au), _p(ap), _p(an), 0, int(off), _p(emb),
-                   emb.stride(0), _p(w), _p(loss), None, 0.0, 0.0, None, None, None, 0, None, _stream())
+            _bpr_call(au.numel(), emb.shape[1], au, ap, an, 0, int(off), emb, w, loss, None, 0.0, 0.0, None, None,
+                      None, 0, None, None)
             aux_loss = loss.mean()
         mask = neighbor_mask(adj, rows) if (adj.reverse() is adj and adj.n_rows == adj.n_cols) else None
         ctx.mask = mask
@@ -705,10 +748,12 @@ class PropagateRows(torch.autograd.Function):
         gs = gb.contiguous() / float(n_layers + 1)
         rs = _prescale(fvals) if feat is not None else None
         mask = ctx.mask
+        keys = rowsort(rows)  # one sort serves the pull and every scatter of this backward
         if adj.reverse() is adj:
             # with L > 1, dx_{L-1} is read only through the first reverse layer's
             # column mask (the neighbour set R): rows off R are not computed
-            dx = spmm_pull(adj, rows, gs, adj_vals, self_add=True, row_mask=mask if n_layers > 1 else None)
+            dx = spmm_pull(adj, rows, gs, adj_vals, self_add=True, row_mask=mask if n_layers > 1 else None,
+                           sorted_keys=keys)
         else:
             dx = torch.zeros(adj.n_cols, gs.shape[1], dtype=torch.float32, device=gs.device)
             spmm_push(adj, rows, gs, dx, adj_vals, self_add=True)
@@ -722,7 +767,8 @@ class PropagateRows(torch.autograd.Function):
                 if (last and rs is not None) or cm is not None:
                     epi = epilogue(row_scale=rs if last else None, col_mask=cm)
                 spmm(at, dx, adj_vals, out=nxt, epi=epi)
-                scatter_add_rows(nxt, rows, gs if not (last and rs is not None) else gs * rs[rows][:, None])
+                scatter_add_rows(nxt, rows, gs if not (last and rs is not None) else gs * rs[rows][:, None],
+                                 sorted_keys=keys)
                 dx, nxt = nxt, dx
         elif rs is not None:
             dx.mul_(rs[:, None])
@@ -741,9 +787,8 @@ class PropagateRows(torch.autograd.Function):
             au, ap, an, off = ctx.aux
             dw = torch.zeros_like(w) if (w is not None and ctx.needs_input_grad[8]) else None
             g_aux = _f32(g_aux).contiguous()
-            L.call('igr_bpr_fwd_bwd_f32', au.numel(), emb.shape[1], _p(au), _p(ap), _p(an), 0, int(off), _p(emb),
-                   emb.stride(0), _p(w), None, None, 1.0 / au.numel(), 0.0, _p(g_aux), None, _p(demb),
-                   demb.stride(0), _p(dw), _stream())
+            _bpr_call(au.numel(), emb.shape[1], au, ap, an, 0, int(off), emb, w, None, None, 1.0 / au.numel(), 0.0,
+                      g_aux, None, demb, demb.stride(0), dw, rowsort(au, 0, ap, int(off), an, int(off)))
         return None, None, None, demb, dfv, None, None, None, dw
 
 
@@ -793,16 +838,17 @@ class BPRLoss(torch.autograd.Function):
     rows gathered from one table t (model.py:4046-4052, trainer.py:536-548)."""
 
     @staticmethod
-    def forward(ctx, t, w, users, pos, neg, off_u, off_i):
+    def forward(ctx, t, w, users, pos, neg, off_u, off_i, distinct):
         _dev(t, users, pos, neg, w)
         t = t.contiguous()
         B = users.numel()
         loss = torch.empty(B, dtype=torch.float32, device=t.device)
         l2 = torch.empty_like(loss)
-        L.call('igr_bpr_fwd_bwd_f32', B, t.shape[1], _p(users), _p(pos), _p(neg), int(off_u), int(off_i), _p(t),
-               t.stride(0), _p(w), _p(loss), _p(l2), 0.0, 0.0, None, None, None, 0, None, _stream())
+        _bpr_call(B, t.shape[1], users, pos, neg, off_u, off_i, t, w, loss, l2, 0.0, 0.0, None, None, None, 0, None,
+                  None)
         ctx.save_for_backward(t, w, users, pos, neg)
         ctx.off = (int(off_u), int(off_i))
+        ctx.distinct = bool(distinct)
         return loss.mean(), l2.mean()
 
     @staticmethod
@@ -814,15 +860,20 @@ class BPRLoss(torch.autograd.Function):
         g2 = None if g_l2 is None else _f32(g_l2).contiguous()
         grad = torch.zeros_like(t) if ctx.needs_input_grad[0] else None
         dw = torch.zeros_like(w) if (w is not None and ctx.needs_input_grad[1]) else None
-        L.call('igr_bpr_fwd_bwd_f32', B, t.shape[1], _p(users), _p(pos), _p(neg), ctx.off[0], ctx.off[1], _p(t),
-               t.stride(0), _p(w), None, None, 0.0 if gl is None else 1.0 / B, 0.0 if g2 is None else 1.0 / B,
-               _p(gl), _p(g2), _p(grad), t.stride(0), _p(dw), _stream())
-        return grad, dw, None, None, None, None, None
+        keys = None
+        if grad is not None and not ctx.distinct:
+            keys = rowsort(users, ctx.off[0], pos, ctx.off[1], neg, ctx.off[1])
+        _bpr_call(B, t.shape[1], users, pos, neg, ctx.off[0], ctx.off[1], t, w, None, None,
+                  0.0 if gl is None else 1.0 / B, 0.0 if g2 is None else 1.0 / B, gl, g2, grad, t.stride(0), dw, keys)
+        return grad, dw, None, None, None, None, None, None
 
 
-def bpr_loss(t, users, pos, neg, off_u, off_i, w=None):
-    """Returns (mean softplus BPR loss, mean squared-norm term)."""
-    return BPRLoss.apply(t, w, users.contiguous(), pos.contiguous(), neg.contiguous(), off_u, off_i)
+def bpr_loss(t, users, pos, neg, off_u, off_i, w=None, distinct=False):
+    """Returns (mean softplus BPR loss, mean squared-norm term).  distinct: the
+    caller guarantees that the 3B table rows read are all different (a table of
+    gathered batch rows read at batch_positions), so the gradient needs no sort."""
+    return BPRLoss.apply(t, w, users.to(torch.int64).contiguous(), pos.to(torch.int64).contiguous(),
+                         neg.to(torch.int64).contiguous(), off_u, off_i, distinct)
 
 
 # ------------------------------------------------------------------ DGL-compatible API

@@ -341,9 +341,17 @@ def graph_epoch(trainer):
     return sg.take_loss() / total
 
 
+def base_seed(trainer_config):
+    """The trainer's sampling seed: config['seed'], or one drawn from torch's seed
+    when the config has none (the reference's configs set none), so that the
+    samplers of one trainer can be given distinct streams derived from it."""
+    seed = trainer_config.get('seed')
+    return int(torch.initial_seed() & 0x7fffffff) if seed is None else int(seed)
+
+
 def make_sampler(trainer_config, dataset, seed):
     if trainer_config.get('sampler', 'device') == 'device' and torch.device(trainer_config['device']).type == 'cuda':
-        return DeviceBPRSampler(dataset, trainer_config['batch_size'], trainer_config['device'], seed or 0)
+        return DeviceBPRSampler(dataset, trainer_config['batch_size'], trainer_config['device'], seed)
     return BPRBatchSampler(dataset, trainer_config['batch_size'], seed)
 
 
@@ -356,7 +364,7 @@ class BPRTrainer(BasicTrainer):
 
     def __init__(self, trainer_config):
         super().__init__(trainer_config)
-        self.sampler = make_sampler(trainer_config, self.dataset, trainer_config.get('seed'))
+        self.sampler = make_sampler(trainer_config, self.dataset, base_seed(trainer_config))
         self.initialize_optimizer()
         self.l2_reg = trainer_config['l2_reg']
         self.fused = trainer_config.get('fused', True)
@@ -394,11 +402,14 @@ class IGCNTrainer(BasicTrainer):
 
     def __init__(self, trainer_config):
         super().__init__(trainer_config)
-        seed = trainer_config.get('seed')
+        # two independent streams, as the reference's two DataLoaders (trainer.py:522-530):
+        # with feature_ratio = 1 the aux dataset IS the dataset, so equal seeds would
+        # train the aux term on exactly the main term's triples
+        seed = base_seed(trainer_config)
         self.sampler = make_sampler(trainer_config, self.dataset, seed)
         self.aux_sampler = make_sampler(trainer_config,
                                         AuxiliaryDataset(self.dataset, self.model.user_map, self.model.item_map),
-                                        None if seed is None else seed + 1)
+                                        seed + 1)
         self.initialize_optimizer()
         self.l2_reg = trainer_config['l2_reg']
         self.aux_reg = trainer_config['aux_reg']

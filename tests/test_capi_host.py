@@ -194,15 +194,25 @@ def test_new_entry_points_validate_arguments():
              match='NULL')
     _refused('igr_spmm_pull_marked_f32', ctypes.byref(multi.csr), 64, F, F, F, F, 64, F, 1.0, 0, None, F, 64, st,
              match='edge_id')
-    _refused('igr_rowset_mark', 4, F, None, F, F, st, match='NULL')
-    _refused('igr_rowset_sum_f32', 4, 64, F, F, F, 32, 1.0, F, 64, st, match='leading')
-    # fused BPR: the LDS dw reduction bounds d; fused dropout: keep in (0, 1]
-    _refused('igr_bpr_fwd_bwd_f32', 4, 2000, F, F, F, 0, 0, F, 2000, F, None, None, 1.0, 0.0, None, None, None, 0,
-             F, st, match='1024')
+    _refused('igr_rowset_mark', 4, F, None, F, st, match='NULL')
+    _refused('igr_rowset_sum_f32', 4, 64, F, F, 32, 1.0, F, F, 64, st, match='leading')
+    _refused('igr_rowset_sum_f32', 4, 64, None, F, 64, 1.0, F, F, 64, st, match='NULL')
+    # fixed-order accumulation: the sort needs its key buffer, the scatter its sorted keys
+    _refused('igr_rowsort', 4, F, 0, None, 0, F, 0, F, st, match='idx2 without idx1')
+    _refused('igr_rowsort', 4, F, 0, None, 0, None, 0, None, st, match='NULL')
+    _refused('igr_scatter_add_rows_f32', 4, 64, None, F, 64, F, 64, st, match='NULL')
+    assert _lib.lib().igr_rowsort_size(0) == 0
+    assert _lib.lib().igr_rowsort_size(6144) == 2 * 6144      # 6 tiles of 1024, ranked in one pass
+    assert _lib.lib().igr_rowsort_size(1000) == 2 * 1024
+    assert _lib.lib().igr_rowsort_size(100 * 1024) == 2 * 128 * 1024  # > 64 tiles: padded to a power of two
+    # fused BPR: the backward needs its workspace; fused dropout: keep in (0, 1]
+    assert _lib.lib().igr_bpr_workspace_floats(2048, 64) == 3 * 2048 * 64 + 128 * 64
+    _refused('igr_bpr_fwd_bwd_f32', 4, 64, F, F, F, 0, 0, F, 64, F, None, None, 1.0, 0.0, None, None, F, 64,
+             None, F, None, st, match='workspace')
     for keep in (0.0, 1.5):
         _refused('igr_spmm_scaled_f32', ctypes.byref(rect.csr), 64, F, 64, None, None, keep, 1, 0, None, 0, F, 64,
                  None, F, st, match='keep')
-    _refused('igr_dropout_uniforms', None, 1, 0, 0, F, st, match='NULL')
+    _refused('igr_dropout_uniforms', None, 1, 0, None, 0, F, st, match='NULL')
     # hipGraph-step entry points: the device counter, Adam's host step without one, per-head SpMM
     _refused('igr_counter_add', None, 1, st, match='NULL')
     _refused('igr_adam_f32', 4, F, F, F, F, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None, st, match='step')

@@ -339,6 +339,73 @@ def test_gather_scatter_and_bpr():
     close(ww.grad.cpu().numpy(), w64.grad.numpy(), rtol=1e-4, atol_row=1e-5)
 
 
+@pytest.mark.parametrize('n,arrays', [(1, 1), (5, 3), (1000, 1), (1024, 1), (1025, 2), (2048, 3), (8192, 1),
+                                      (2731, 3), (70001, 1), (40000, 3)])
+def test_rowsort_is_a_stable_sort_by_row(n, arrays):
+    """keys = (row << 32 | entry) ascending == numpy's stable sort of the rows:
+    one tile, several tiles ranked in LDS / in global memory, and > 64 tiles
+    (pairwise merges first)."""
+    rng = np.random.default_rng(n + arrays)
+    hi = max(3, n // 7)  # many repeats
+    idx = [rng.integers(0, hi, n) for _ in range(arrays)]
+    offs = [0, 1000, 5][:arrays]
+    args = []
+    for a, o in zip(idx, offs):
+        args += [t(a), o]
+    keys = ops.rowsort(*args).cpu().numpy().astype(np.uint64)
+    rows = np.concatenate([a + o for a, o in zip(idx, offs)]).astype(np.uint64)
+    order = np.argsort(rows, kind='stable').astype(np.uint64)
+    total = n * arrays
+    np.testing.assert_array_equal(keys[:total], (rows[order] << np.uint64(32)) | order)
+
+
+@pytest.mark.parametrize('d', [64, 128, 20])
+def test_scatter_add_rows_equals_sequential_index_add_bitwise(d):
+    """dst[idx[i]] += src[i] in increasing i per row: the order of a sequential
+    loop over i (torch's CPU index_add_, and its index_put(accumulate=True) - the
+    reference's gather backward - on one thread), hence the same bits."""
+    rng = np.random.default_rng(d)
+    n, rows = 6144, 900
+    idx = rng.integers(0, 40, n)  # heavy repeats
+    idx[n // 2:] = rng.integers(0, rows - 7, n - n // 2)
+    src = rng.standard_normal((n, d)).astype(np.float32)
+    dst0 = rng.standard_normal((rows, d)).astype(np.float32)
+    ref = torch.from_numpy(dst0.copy())
+    ref.index_add_(0, torch.from_numpy(idx + 7), torch.from_numpy(src))
+    out = ops.scatter_add_rows(t(dst0.copy()), t(idx), t(src), offset=7)
+    assert torch.equal(out.cpu(), ref)
+    again = ops.scatter_add_rows(t(dst0.copy()), t(idx), t(src), offset=7)
+    assert torch.equal(out, again)
+
+
+def test_bpr_gradient_fixed_order():
+    """The fused BPR gradient with repeated rows: bitwise equal run to run, equal
+    to the distinct-rows form applied to gathered copies and scattered back in
+    entry order, and dw bitwise equal run to run."""
+    rng = np.random.default_rng(77)
+    B, d = 2048, 64
+    T = rng.standard_normal((600, d)).astype(np.float32)
+    w = rng.random(d).astype(np.float32) + 0.5
+    users, pos, neg = rng.integers(0, 150, B), rng.integers(0, 60, B), rng.integers(0, 400, B)
+    runs = []
+    for _ in range(2):
+        tt, ww = t(T).requires_grad_(True), t(w).requires_grad_(True)
+        loss, l2 = ops.bpr_loss(tt, t(users), t(pos), t(neg), 0, 200, w=ww)
+        (loss + 0.3 * l2).backward()
+        runs.append((tt.grad.clone(), ww.grad.clone()))
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
+    # the same terms through a table of gathered rows (all distinct), scattered in entry order
+    rows = np.concatenate([users, 200 + pos, 200 + neg])
+    gt = t(T[rows]).requires_grad_(True)
+    iu, ip, ineg = ops.batch_positions(B, DEV)
+    ww = t(w).requires_grad_(True)
+    loss, l2 = ops.bpr_loss(gt, iu, ip, ineg, 0, 0, w=ww, distinct=True)
+    (loss + 0.3 * l2).backward()
+    back = ops.scatter_add_rows(torch.zeros(600, d, device=DEV), t(rows), gt.grad)
+    assert torch.equal(back, runs[0][0])
+    assert torch.equal(ww.grad, runs[0][1])
+
+
 def test_edge_dropout_and_feat_values(golden):
     nu, ni, ta = int(golden['n_users']), int(golden['n_items']), golden['train_array']
     F = O.generate_feat(nu, ni, ta)
@@ -464,6 +531,35 @@ def test_device_sampler_semantics():
     b = s.sample(1000, offset=7)
     c = s.sample(1000, offset=8)
     assert all(torch.equal(x, y) for x, y in zip(a, b)) and not torch.equal(a[2], c[2])
+
+
+def test_device_sampler_heavy_user_gets_true_negative():
+    """A user who interacted with all but two items: when the rejection rounds run
+    out the negative is drawn from the complement directly, never a positive."""
+    from igr.sampler import DeviceBPRSampler
+    ni, free = 120, [17, 93]
+    items = [i for i in range(ni) if i not in free]
+    pairs = np.stack([np.zeros(len(items), np.int64), np.array(items)], 1)
+
+    class DS:
+        n_users, n_items, train_pairs = 1, ni, pairs
+
+        def __len__(self):
+            return len(pairs)
+    s = DeviceBPRSampler(DS(), 4096, DEV, seed=5, max_rounds=1)
+    _, _, n = (x.cpu().numpy() for x in s.sample(20000))
+    assert set(np.unique(n).tolist()) == set(free)
+    share = float((n == free[0]).mean())
+    assert 0.45 < share < 0.55
+
+
+def test_feat_values_rejects_stale_buffers():
+    g, _ = rand_graph(50, 40, 300, seed=1)
+    rs = torch.ones(50, device=DEV)
+    with pytest.raises(ops.IgrError, match='edges'):
+        ops.feat_values(g, rs, -0.5, out=torch.empty(g.nnz - 1, device=DEV))
+    with pytest.raises(ops.IgrError, match='rows'):
+        ops.feat_row_values(rs, -0.5, out=torch.empty(49, device=DEV))
 
 
 @pytest.mark.parametrize('d', [32, 64, 128, 256])

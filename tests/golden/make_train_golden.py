@@ -101,12 +101,12 @@ def run(shape):
     import model as ref_model
     import trainer as ref_trainer
     nu, ni, mean_deg, d, L, epochs = ml_like.SHAPES[shape]
-    train, val, test = ml_like.make_splits(nu, ni, mean_deg, seed=100)
+    train, val, test = ml_like.splits_for(shape)
     ds = DS(shape, nu, ni, train, val, test)
     bs = 2048
     spe = ml_like.steps_per_epoch(train, bs)
-    main_b = ml_like.batches(train, ni, bs, spe * epochs, seed=1)
-    aux_b = ml_like.batches(train, ni, bs, spe * epochs, seed=2)  # feature_ratio = 1: aux maps are identity
+    main_b = ml_like.batches_for(shape, train, ni, bs, spe * epochs, seed=1)
+    aux_b = ml_like.batches_for(shape, train, ni, bs, spe * epochs, seed=2)  # feature_ratio = 1: aux maps are identity
     torch.manual_seed(7)
     cfg = {'name': 'IGCN', 'embedding_size': d, 'n_layers': L, 'device': 'cpu', 'dropout': 0.3,
            'feature_ratio': 1., 'dataset': ds}
@@ -170,11 +170,11 @@ def run_lightgcn(shape, l2_reg=1e-4):
     import model as ref_model
     import trainer as ref_trainer
     nu, ni, mean_deg, d, L, epochs = ml_like.SHAPES[shape]
-    train, val, test = ml_like.make_splits(nu, ni, mean_deg, seed=100)
+    train, val, test = ml_like.splits_for(shape)
     ds = DS(shape, nu, ni, train, val, test)
     bs = 2048
     spe = ml_like.steps_per_epoch(train, bs)
-    main_b = ml_like.batches(train, ni, bs, spe * epochs, seed=1)
+    main_b = ml_like.batches_for(shape, train, ni, bs, spe * epochs, seed=1)
     torch.manual_seed(11)
     m = ref_model.LightGCN({'name': 'LightGCN', 'embedding_size': d, 'n_layers': L, 'device': 'cpu',
                             'dataset': ds})

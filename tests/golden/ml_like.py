@@ -22,6 +22,118 @@ SHAPES = {
 }
 
 
+# The Gowalla shape of BASELINE's third configuration (29,858 users x 40,981 items,
+# ~1.03 M training interactions, d = 128, 3 layers; /root/reference config.py:12-23):
+# (n_users, n_items, mean interactions per user, d, n_layers, epochs)
+SHAPES['gowalla'] = (29858, 40981, 43, 128, 3, 2)
+
+
+def zipf_splits(n_users, n_items, mean_deg, seed, min_deg=10):
+    """Vectorised synthetic interactions for shapes too large for make_splits'
+    dense preference matrix: per-user lognormal activity (>= min_deg, Gowalla's
+    10-core), items drawn from a Zipf(0.9) popularity law (repeats dropped), a
+    random interaction-time order per user and the same per-user 80/10/10 split
+    (dataset.py:94-114).  Returns (train, val, test) lists of sorted item lists."""
+    rng = np.random.default_rng(seed)
+    deg = np.clip(rng.lognormal(np.log(mean_deg) - 0.3, 0.8, n_users), min_deg, n_items // 4).astype(np.int64)
+    w = 1.0 / np.arange(1, n_items + 1) ** 0.9
+    perm = rng.permutation(n_items)
+    # draw 30 % extra so that most users still reach their degree after repeats are dropped
+    draws = (deg * 1.3).astype(np.int64) + 2
+    u = np.repeat(np.arange(n_users, dtype=np.int64), draws)
+    i = perm[rng.choice(n_items, size=int(draws.sum()), p=w / w.sum())]
+    key = np.unique(u * n_items + i)
+    u, i = key // n_items, key % n_items
+    t = rng.random(len(u))  # synthetic interaction time
+    order = np.lexsort((t, u))
+    u, i = u[order], i[order]
+    ptr = np.searchsorted(u, np.arange(n_users + 1))
+    train, val, test = [], [], []
+    for x in range(n_users):
+        items = i[ptr[x]:ptr[x + 1]][:deg[x]]
+        n_tr, n_te = int(len(items) * 0.8), int(len(items) * 0.1)
+        train.append(sorted(items[:n_tr].tolist()))
+        val.append(sorted(items[n_tr:len(items) - n_te].tolist()))
+        test.append(sorted(items[len(items) - n_te:].tolist()))
+    return train, val, test
+
+
+def batches_vec(train_data, n_items, batch_size, n_steps, seed):
+    """batches() for large shapes, vectorised: the same distribution (user uniform
+    over users with training items, positive uniform over the user's items,
+    negative uniform over the items the user has not interacted with, by
+    rejection; dataset.py:119-131)."""
+    rng = np.random.default_rng(seed)
+    lens = np.array([len(x) for x in train_data], np.int64)
+    ptr = np.concatenate([[0], np.cumsum(lens)])
+    flat = np.fromiter((i for x in train_data for i in x), np.int64, count=int(ptr[-1]))
+    users_ok = np.nonzero(lens > 0)[0].astype(np.int64)
+    keys = np.repeat(np.arange(len(train_data), dtype=np.int64), lens) * n_items + flat  # sorted
+    out = []
+    for _ in range(n_steps):
+        u = users_ok[rng.integers(0, len(users_ok), batch_size)]
+        p = flat[ptr[u] + (rng.random(batch_size) * lens[u]).astype(np.int64)]
+        n = rng.integers(0, n_items, batch_size)
+        while True:
+            k = u * n_items + n
+            j = np.minimum(np.searchsorted(keys, k), len(keys) - 1)
+            bad = np.nonzero(keys[j] == k)[0]
+            if len(bad) == 0:
+                break
+            n[bad] = rng.integers(0, n_items, len(bad))
+        out.append((u, p, n))
+    return out
+
+
+def splits_for(shape, seed=100):
+    """The (train, val, test) lists of a named shape."""
+    nu, ni, mean_deg = SHAPES[shape][:3]
+    return zipf_splits(nu, ni, mean_deg, seed) if shape == 'gowalla' else make_splits(nu, ni, mean_deg, seed)
+
+
+def batches_for(shape, train_data, n_items, batch_size, n_steps, seed):
+    fn = batches_vec if shape == 'gowalla' else batches
+    return fn(train_data, n_items, batch_size, n_steps, seed)
+
+
+def _name_seed(name):
+    import zlib
+    return zlib.crc32(name.encode()) & 0x7fffffff
+
+
+def scale_params(name, n_rows, d, heads=0):
+    """Model parameters of a BASELINE-sized fixture (tests/golden/make_scale_golden.py):
+    numpy legacy streams, identical wherever they are drawn.  emb ~ N(0, 0.1^2)
+    (model.py:4124); with heads, the d -> heads * d projections of AttIGCN drawn
+    as nn.Linear draws them, U(-1/sqrt(d), 1/sqrt(d))."""
+    rs = np.random.RandomState(_name_seed(name))
+    P = {'emb': (rs.standard_normal((n_rows, d)) * 0.1).astype(np.float32)}
+    if heads:
+        b = 1.0 / np.sqrt(d)
+        for k, shp in [('wq', (heads * d, d)), ('bq', (heads * d,)), ('wk', (heads * d, d)), ('bk', (heads * d,))]:
+            P[k] = rs.uniform(-b, b, shp).astype(np.float32)
+    return P
+
+
+def scale_samples(name, n_nodes, nnz_feat, nnz_adj=None):
+    """The rows / edges whose values a BASELINE-sized fixture keeps: 512 node rows,
+    512 rows of the feature table (its last two, the general features every node
+    reads, always among them), 4096 edges of the feature graph (and of the
+    adjacency)."""
+    rs = np.random.RandomState(_name_seed(name) ^ 0x5bd1e995)
+    rows = np.unique(np.concatenate([[0, n_nodes - 1], rs.randint(0, n_nodes, 510)]))
+    feat_rows = np.unique(np.concatenate([[0, n_nodes, n_nodes + 1], rs.randint(0, n_nodes + 2, 509)]))
+    out = {'rows': rows, 'feat_rows': feat_rows, 'edges': np.unique(rs.randint(0, nnz_feat, 4096))}
+    if nnz_adj is not None:
+        out['adj_edges'] = np.unique(rs.randint(0, nnz_adj, 4096))
+    return out
+
+
+def scale_cotangent(shape):
+    """The fixed cotangent R of the gradient fixtures: gradients of sum(rep * R)."""
+    return np.random.RandomState(8).standard_normal(shape).astype(np.float32)
+
+
 def make_splits(n_users, n_items, mean_deg, seed):
     rng = np.random.default_rng(seed)
     P = rng.normal(size=(n_users, 8))

@@ -1,0 +1,279 @@
+"""GPU parity at the size of BASELINE's configurations (not only toy graphs).
+
+    MovieLens-1M shape, d = 64, 2 layers, attention SpMM   AttIGCN  model.py:4223-4287
+    Gowalla shape (29,858 x 40,981, ~1.04 M), d = 128, L = 3  IGCN     model.py:4188-4200, config.py:12-23
+    synthetic scale, d = 256, the sharded layer with 128-column passes
+    items outnumbering users (Amazon-Books-shaped), items sharded at world 2 on one GPU
+
+The first two compare against fixtures written by tests/golden/make_scale_golden.py,
+which RAN the reference on the same inputs (data from tests/golden/ml_like.py,
+parameters from numpy streams; the fixtures keep float64 column sums and sampled
+rows), and against the CPU oracle.  Tolerances as in test_gpu_models: 1e-5
+relative + 1e-6 of the row max for SpMM-type outputs (3e-5 / 3e-6 through the
+attention softmax), 1e-4 / 1e-5 for gradients through it; index arrays exact.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN
+from igr import model as M
+from oracle import igr_oracle as O
+from test_gpu_kernels import close
+
+sys.path.insert(0, GOLDEN)
+import ml_like  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda')
+
+
+class DS:
+    def __init__(self, name, n_users, n_items, train):
+        self.name, self.n_users, self.n_items = name, n_users, n_items
+        self.train_data = train
+        lens = np.array([len(x) for x in train], np.int64)
+        flat = np.fromiter((i for x in train for i in x), np.int64, count=int(lens.sum()))
+        self.train_pairs = np.stack([np.repeat(np.arange(n_users, dtype=np.int64), lens), flat], 1)
+        self.train_array = self.train_pairs
+
+    def __len__(self):
+        return len(self.train_pairs)
+
+
+def _load(name):
+    path = os.path.join(GOLDEN, name)
+    if not os.path.exists(path):
+        pytest.skip(f'{path} not generated')
+    return np.load(path)
+
+
+def check_summary(fx, key, t, rows, rtol=1e-5, atol_row=1e-6, sum_tol=2e-6):
+    """Sampled rows against the reference's, and the float64 column sums of the
+    whole tensor within sum_tol of its sum of magnitudes."""
+    a = t.detach().cpu().numpy()
+    close(a[rows], fx[key + '_rows'], rtol=rtol, atol_row=atol_row)
+    cs = a.astype(np.float64).sum(0)
+    assert np.abs(cs - fx[key + '_colsum']).max() <= sum_tol * float(fx[key + '_abssum']), key
+    assert float(np.abs(a.astype(np.float64)).sum()) == pytest.approx(float(fx[key + '_abssum']), rel=1e-5)
+
+
+def test_attigcn_at_ml1m_shape_matches_reference():
+    """BASELINE configuration 2: attention SpMM at the MovieLens-1M shape, d = 64, L = 2."""
+    fx = _load('scale_att_ml1m.npz')
+    nu, ni, _, d, L, _ = ml_like.SHAPES['ml1m']
+    train, _, _ = ml_like.splits_for('ml1m')
+    ds = DS('ml1m', nu, ni, train)
+    assert len(ds) == int(fx['n_train'])
+    cfg = {'name': 'AttIGCN', 'embedding_size': d, 'n_layers': L, 'device': DEV, 'dropout': 0.3,
+           'feature_ratio': 1., 'dataset': ds, 'dropout_rng': 'cpu'}
+    m = M.AttIGCN(cfg)
+    assert m.feat_mat.nnz == int(fx['nnz_feat'])
+    P = ml_like.scale_params('att_ml1m', m.embedding.weight.shape[0], d, heads=4)
+    S = ml_like.scale_samples('att_ml1m', nu + ni, m.feat_mat.nnz)
+    with torch.no_grad():
+        m.embedding.weight.copy_(torch.from_numpy(P['emb']))
+        for lin, w, b in [(m.weight_q, 'wq', 'bq'), (m.weight_k, 'wk', 'bk')]:
+            lin.weight.copy_(torch.from_numpy(P[w]))
+            lin.bias.copy_(torch.from_numpy(P[b]))
+    m.eval()
+    with torch.no_grad():
+        alpha = m.inductive_rep_layer(m.feat_vals, return_alpha=True)
+        close(alpha.cpu().numpy()[S['edges']], fx['alpha_edges'], rtol=3e-5, atol_row=2e-6)
+        assert float(alpha.double().sum()) == pytest.approx(float(fx['alpha_sum']), rel=1e-6)
+        x0 = m.inductive_rep_layer(m.feat_vals)
+        check_summary(fx, 'x0', x0, S['rows'], rtol=3e-5, atol_row=3e-6)
+    # the CPU oracle's restatement of the same layer (model.py:4257-4281) on the full graph
+    F = O.generate_feat(nu, ni, ds.train_pairs)
+    fv = O.feat_values(F, 0.0)
+    np.testing.assert_array_equal(m.feat_mat.host()['col_idx'], F.col.astype(np.int32))
+    x0_o, w_o = O.att_x0(F, fv, P['emb'], P['wq'], P['bq'], P['wk'], P['bk'])
+    close(alpha.cpu().numpy(), w_o, rtol=3e-5, atol_row=2e-6)
+    close(x0.cpu().numpy(), x0_o, rtol=3e-5, atol_row=3e-6)
+    rep = m.get_rep()
+    check_summary(fx, 'rep', rep, S['rows'], rtol=3e-5, atol_row=3e-6)
+    R = torch.from_numpy(ml_like.scale_cotangent(tuple(rep.shape))).to(DEV)
+    (rep * R).sum().backward()
+    check_summary(fx, 'grad_emb', m.embedding.weight.grad, S['feat_rows'], rtol=1e-4, atol_row=1e-5, sum_tol=1e-5)
+    for g, k in [(m.weight_q.weight.grad, 'grad_wq'), (m.weight_k.weight.grad, 'grad_wk')]:
+        ref = fx[k].astype(np.float64)
+        assert np.abs(g.cpu().numpy() - ref).max() <= 1e-4 * np.abs(ref).max(), k
+    assert np.abs(m.weight_q.bias.grad.cpu().numpy() - fx['grad_bq']).max() <= 1e-4 * np.abs(fx['grad_bq']).max()
+    # train mode: the reference's own dropout draws (CPU generator); dropped edges leave the softmax
+    m.train()
+    torch.manual_seed(33)
+    with torch.no_grad():
+        check_summary(fx, 'train_rep', m.get_rep(), S['rows'], rtol=3e-5, atol_row=3e-6)
+
+
+def test_igcn_at_gowalla_shape_matches_reference():
+    """BASELINE configuration 3: IGCN at the Gowalla shape, d = 128, L = 3 (config.py:12-23)."""
+    fx = _load('scale_igcn_gowalla.npz')
+    nu, ni, _, d, L, _ = ml_like.SHAPES['gowalla']
+    train, _, _ = ml_like.splits_for('gowalla')
+    ds = DS('gowalla', nu, ni, train)
+    assert len(ds) == int(fx['n_train'])
+    m = M.IGCN({'name': 'IGCN', 'embedding_size': d, 'n_layers': L, 'device': DEV, 'dropout': 0.3,
+                'feature_ratio': 1., 'dataset': ds, 'dropout_rng': 'cpu'})
+    assert m.feat_mat.nnz == int(fx['nnz_feat']) and m.norm_adj.nnz == int(fx['nnz_adj'])
+    P = ml_like.scale_params('igcn_gowalla', m.embedding.weight.shape[0], d)
+    S = ml_like.scale_samples('igcn_gowalla', nu + ni, m.feat_mat.nnz, m.norm_adj.nnz)
+    # degree / normalisation work: bit-exact against the reference's values
+    np.testing.assert_array_equal(m.norm_vals.cpu().numpy()[S['adj_edges']], fx['norm_val_edges'])
+    assert float(m.norm_vals.double().sum()) == float(fx['norm_val_sum'])
+    with torch.no_grad():
+        m.embedding.weight.copy_(torch.from_numpy(P['emb']))
+    m.eval()
+    rep = m.get_rep()
+    check_summary(fx, 'rep', rep, S['rows'])
+    # float64 oracle on the whole graph
+    A, F = O.norm_adj(nu, ni, ds.train_pairs), O.generate_feat(nu, ni, ds.train_pairs)
+    x = O.spmm64(F, P['emb'], val=O.feat_values(F, 1.0))
+    acc = x.copy()
+    for _ in range(L):
+        x = _spmm64_f64(A, x)
+        acc += x
+    close(rep.detach().cpu().numpy(), acc / (L + 1), rtol=1e-5, atol_row=2e-6)
+    (rep * torch.from_numpy(ml_like.scale_cotangent(tuple(rep.shape))).to(DEV)).sum().backward()
+    check_summary(fx, 'grad_emb', m.embedding.weight.grad, S['feat_rows'], rtol=2e-5, atol_row=2e-6, sum_tol=1e-5)
+    m.train()
+    torch.manual_seed(31)
+    with torch.no_grad():
+        check_summary(fx, 'train_rep', m.get_rep(), S['rows'])
+
+
+def _spmm64_f64(A, x64):
+    """A x with float64 input (scipy): the layers of the float64 reference chain."""
+    import scipy.sparse as sp
+    mat = sp.csr_matrix((A.val.astype(np.float64), A.col, A.row_ptr), shape=(A.n_rows, A.n_cols))
+    return mat @ x64
+
+
+def test_sharded_layer_d256_column_passes_at_scale():
+    """BASELINE configuration 5's layer (d = 256) on one GPU at a size where the item
+    table (300 K x 1 KB = 307 MB) outgrows the Infinity Cache, so both sides run as two
+    128-column passes: float64 spot rows, linearity of the whole layer, and bitwise
+    equality with the single-pass path."""
+    from igr import dist
+    from igr.dataset import synthetic_pairs
+    U, I, E, d = 1_000_000, 300_000, 20_000_000, 256
+    pairs = synthetic_pairs(U, I, E, 5, 'uniform')
+    sh = dist.BipartiteShard(pairs, U, I, 0, 1, DEV, d=d, item_tiles=2)
+    assert dist._col_width(d, I * d * 4) == 128
+    g = torch.Generator(device=DEV).manual_seed(1)
+    xu, xi = torch.randn(U, d, generator=g, device=DEV) * 0.1, torch.randn(I, d, generator=g, device=DEV) * 0.1
+    yu, yi = sh.layer(xu, xi)
+    # float64 on sampled rows of both sides
+    rng = np.random.default_rng(0)
+    ub, ih = sh.user_block.host(), sh.item_host
+    xi_h, xu_h = xi.cpu().numpy().astype(np.float64), xu.cpu().numpy().astype(np.float64)
+    uv, iv = sh.user_vals.cpu().numpy().astype(np.float64), ih['vals'].astype(np.float64)
+    for r in rng.integers(0, U, 64):
+        b, e = ub['row_ptr'][r], ub['row_ptr'][r + 1]
+        close(yu[r].cpu().numpy()[None], (uv[b:e, None] * xi_h[ub['col_idx'][b:e]]).sum(0)[None])
+    for r in rng.integers(0, I, 64):
+        b, e = ih['row_ptr'][r], ih['row_ptr'][r + 1]
+        close(yi[r].cpu().numpy()[None], (iv[b:e, None] * xu_h[ih['col_idx'][b:e]]).sum(0)[None], atol_row=2e-6)
+    # linearity: layer(a x + b z) == a layer(x) + b layer(z) to rounding
+    zu, zi = torch.randn(U, d, generator=g, device=DEV) * 0.1, torch.randn(I, d, generator=g, device=DEV) * 0.1
+    wu, wi = sh.layer(zu, zi)
+    cu, ci = sh.layer(0.5 * xu - 2.0 * zu, 0.5 * xi - 2.0 * zi)
+    for got, a, b in [(cu, yu, wu), (ci, yi, wi)]:
+        ref = 0.5 * a.double() - 2.0 * b.double()
+        scale = float(ref.abs().max())
+        assert float((got.double() - ref).abs().max()) <= 2e-6 * scale
+    # the column passes change no bit
+    one = dist._col_width
+    try:
+        dist._col_width = lambda d_, table_bytes: d_
+        vu, vi = sh.layer(xu, xi)
+    finally:
+        dist._col_width = one
+    assert torch.equal(vu, yu) and torch.equal(vi, yi)
+
+
+# ---------------------------------------------------------------- items outnumber users, items sharded (world 2)
+
+AM_U, AM_I, AM_E, AM_D = 52_000, 290_000, 3_000_000, 128
+
+
+def _amazon_pairs():
+    from igr.dataset import synthetic_pairs
+    return synthetic_pairs(AM_U, AM_I, AM_E, 9, 'zipf')
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _am_rank(rank, world, port, q):
+    import torch.distributed as tdist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    tdist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from igr.dist import BipartiteShard, sharded_side
+        dev = torch.device('cuda')
+        pairs = _amazon_pairs()
+        side = sharded_side(AM_U, AM_I, 'auto')
+        assert side == 'items'
+        sw = np.ascontiguousarray(pairs[:, ::-1])  # the shard cuts its first side: items
+        sh = BipartiteShard(sw, AM_I, AM_U, rank, world, dev, d=AM_D)
+        rng = np.random.default_rng(3)
+        x_items = (rng.standard_normal((AM_I, AM_D)) * 0.1).astype(np.float32)
+        x_users = (rng.standard_normal((AM_U, AM_D)) * 0.1).astype(np.float32)
+        y_own, y_rep = sh.layer(torch.from_numpy(x_items[sh.u0:sh.u1]).to(dev), torch.from_numpy(x_users).to(dev))
+        y1_own, y1_rep = sh.propagate(torch.from_numpy(x_items[sh.u0:sh.u1]).to(dev),
+                                      torch.from_numpy(x_users).to(dev), 2)
+        torch.cuda.synchronize()
+        q.put((rank, sh.u0, sh.u1, y_own.cpu().numpy(), y_rep.cpu().numpy(), y1_own.cpu().numpy(),
+               y1_rep.cpu().numpy()))
+    except Exception:
+        import traceback
+        q.put((rank, 'error', traceback.format_exc(), None, None, None, None))
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_items_sharded_world2_one_gpu_matches_oracle():
+    """BASELINE configuration 4's partition: items outnumber users (Amazon-Books-shaped,
+    dataset.py:229-255), so the ITEMS are cut into ranges and the user block is
+    replicated and all-reduced.  Two ranks on one GPU (gloo, host-staged), one layer
+    and two chained layers, against the float64 oracle of D^-1/2 A D^-1/2."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_am_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=120)
+    for r in res:
+        assert r[1] != 'error', r[2]
+    pairs = _amazon_pairs()
+    A = O.norm_adj(AM_U, AM_I, pairs)  # rows [users; items]
+    rng = np.random.default_rng(3)
+    x_items = (rng.standard_normal((AM_I, AM_D)) * 0.1).astype(np.float32)
+    x_users = (rng.standard_normal((AM_U, AM_D)) * 0.1).astype(np.float32)
+    x = np.concatenate([x_users, x_items])
+    y = O.spmm64(A, x)
+    y2 = _spmm64_f64(A, y)
+    assert res[0][1] == 0 and res[-1][2] == AM_I and res[0][2] == res[1][1]
+    for rank, i0, i1, y_own, y_rep, y2_own, y2_rep in res:
+        close(y_own, y[AM_U + i0:AM_U + i1], atol_row=2e-6)
+        close(y_rep, y[:AM_U], atol_row=2e-6)       # the replicated user block, all-reduced
+        close(y2_own, y2[AM_U + i0:AM_U + i1], rtol=2e-5, atol_row=3e-6)
+        close(y2_rep, y2[:AM_U], rtol=2e-5, atol_row=3e-6)
+    # both ranks hold the same reduced user block, bit for bit
+    assert np.array_equal(res[0][4], res[1][4]) and np.array_equal(res[0][6], res[1][6])

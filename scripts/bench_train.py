@@ -33,6 +33,9 @@ def main():
     ap.add_argument('--model', default='IGCN', choices=['IGCN', 'AttIGCN', 'LightGCN'])
     ap.add_argument('--eval', action='store_true', help='also time one full eval ranking (Recall@20 path)')
     ap.add_argument('--graph', action='store_true', help='replay one hipGraph-captured step (trainer.StepGraph)')
+    ap.add_argument('--dist-backend', default='nccl', help="'nccl' (= RCCL); 'gloo' for rehearsals (host-staged)")
+    ap.add_argument('--one-device', action='store_true',
+                    help='every rank on cuda:0 (multi-rank rehearsal on a one-GPU box, with --dist-backend gloo)')
     ap.add_argument('--sharded', action='store_true',
                     help='igr.dist_train.ShardedIGCN (one rank per GPU under torch.distributed.run; '
                          'per-rank batch --batch)')
@@ -44,8 +47,12 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     if args.sharded and world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', '0')))
-        dist.init_process_group('nccl', device_id=torch.device('cuda', int(os.environ.get('LOCAL_RANK', '0'))))
+        local = 0 if args.one_device else int(os.environ.get('LOCAL_RANK', '0'))
+        torch.cuda.set_device(local)
+        if args.dist_backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(args.dist_backend)
     dev = torch.device('cuda')
     import threading
     building = threading.Event()
@@ -150,11 +157,12 @@ def sharded(args, ds, rank, world, dev):
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], device=dev)
+        t = torch.tensor([el], device=dev if args.dist_backend == 'nccl' else 'cpu')  # gloo: CPU tensors only
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
     if rank == 0:
-        print(json.dumps({'mode': 'sharded', 'world': world, 'ms_per_step': el / args.steps * 1e3,
+        print(json.dumps({'mode': 'sharded', 'world': world, 'backend': args.dist_backend,
+                          'one_device': args.one_device, 'ms_per_step': el / args.steps * 1e3,
                           'samples_per_s': world * args.batch * args.steps / el, 'loss': float(loss),
                           'n_users': args.n_users, 'n_items': args.n_items, 'n_edges': args.n_edges, 'd': args.d,
                           'layers': args.layers}))

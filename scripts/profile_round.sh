@@ -5,7 +5,7 @@
 set -euo pipefail
 TAG=${1:-r01}
 shift || true
-ARGS=${@:---steps 10 --warmup 3 --cpu-seconds 0}
+ARGS=${@:---steps 10 --warmup 3 --cpu-passes 0}
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"

@@ -76,4 +76,4 @@ Command: `scripts/profile_round.sh {tag}` on one MI355X (rocprofv3, separate tra
 
 
 if __name__ == '__main__':
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else 'd64_U10000000_I1000000_E200000000_w1_T4')
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else 'd64_U10000000_I1000000_E200000000_uniform_w1_T4')

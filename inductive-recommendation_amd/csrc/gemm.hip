@@ -8,6 +8,9 @@
 // (M, N = d..4d, K = node count) have only a few output tiles: there K is
 // split over workgroups (grid.z) into a workspace and summed in split order.  f32-input MFMA is an exact
 // k-ordered fmaf chain (no xf32 on gfx950), i.e. fp32 semantics.
+#include <algorithm>
+#include <type_traits>
+
 #include "common.h"
 
 namespace igr {
@@ -253,6 +256,134 @@ __global__ __launch_bounds__(256) void gemm128_f32_mfma(int64_t M, int64_t N, in
     }
 }
 
+// Tall-and-skinny projection with the WEIGHT HELD IN REGISTERS:
+//   C[M, N] = A[M, K] W^T + bias,  K in {32, 64}, N a multiple of 64, M = node count
+// (AttIGCN's Linear(d, 4d) over every node, model.py:4259, 4264; NGCF's Linear(d, d),
+// model.py:4039).  With K this short a conventional tile has only K / 16 steps to
+// hide its first loads and its C epilogue behind; here a workgroup is persistent
+// over 64-row tiles of A instead:
+//  * each wave owns 16 NB output columns and keeps its slice of W as MFMA
+//    operands in K/4 * NB registers for the whole launch (W never touches LDS);
+//  * the MFMA is issued transposed, D = W_slice (16 x 4) x A_tile^T (4 x 16), so a
+//    lane ends up with FOUR CONSECUTIVE COLUMNS of one output row: C leaves the
+//    registers as 16-byte stores with no LDS staging;
+//  * A tiles go global -> registers -> LDS (double-buffered, the next tile's loads
+//    issued before this tile's MFMAs and written to LDS after them, one barrier per
+//    tile), stride K + 4 floats so
+//    both the 16-byte staging stores and the operand reads are bank-conflict free;
+//  * bias is the accumulators' initial value.
+// Two workgroups per CU: one wave's loads / stores overlap the other's MFMAs.
+template <int KS, int NB, bool TB>
+__global__ __launch_bounds__(256, 2) void gemm_rows_persistent(int64_t M, const float *__restrict__ A, int64_t lda,
+                                                              const float *__restrict__ B, int64_t ldb,
+                                                              const float *__restrict__ bias,
+                                                              float *__restrict__ C, int64_t ldc) {
+    constexpr int K = KS * 4, TM = 64, STR = K + 4;
+    constexpr int LP = TM * K / 4 / 256;  // float4 per thread per A tile
+    __shared__ __align__(16) float As[2][TM * STR];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int m16 = lane & 15, g = lane >> 4;
+    const int64_t n0 = (int64_t)blockIdx.y * (64 * NB) + wave * (16 * NB);
+    float w[NB][KS];
+    f32x4 bz[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const int64_t n = n0 + 16 * j + m16;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int k = 4 * ks + g;
+            w[j][ks] = TB ? B[(int64_t)k * ldb + n] : B[n * ldb + k];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bz[j][r] = bias ? bias[n0 + 16 * j + 4 * g + r] : 0.f;
+    }
+    float4 ra[LP];
+    // GUARD = false: the tile lies wholly inside M - straight-line code, so the
+    // compiler can count the memory operations in flight exactly
+    auto load = [&](int64_t m0, auto guard) {
+#pragma unroll
+        for (int i = 0; i < LP; ++i) {
+            const int idx = t + i * 256;
+            const int64_t gm = m0 + idx / (K / 4);
+            if (!decltype(guard)::value || gm < M)
+                ra[i] = *reinterpret_cast<const float4 *>(A + gm * lda + (idx % (K / 4)) * 4);
+            else
+                ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto stage = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < LP; ++i) {
+            const int idx = t + i * 256;
+            *reinterpret_cast<float4 *>(&As[buf][(idx / (K / 4)) * STR + (idx % (K / 4)) * 4]) = ra[i];
+        }
+    };
+    const int64_t n_tiles = (M + TM - 1) / TM, full_tiles = M / TM;
+    int64_t tile = blockIdx.x;
+    if (tile < n_tiles) {
+        load(tile * TM, std::true_type{});
+        stage(0);
+    }
+    // Every load above (the weight slice, the bias) completes HERE.  Left to the first
+    // use inside the loop, the wait would sit in the loop body and, counting memory
+    // operations in order, would there also cover the A loads and C stores of every
+    // iteration: no overlap at all.
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    int buf = 0;
+    // A tile is computed as two halves of 32 rows, each with its own accumulators, in
+    // the order: next tile's loads, half 0, stores 0, half 1, next tile into the other
+    // LDS buffer, stores 1, barrier.  The only wait on memory is the one before the
+    // next tile goes to LDS; memory operations retire in order and the loads are older
+    // than stores 0, so it leaves those stores in flight: C drains under the MFMAs.
+    auto body = [&](auto guard) {
+        constexpr bool GUARD = decltype(guard)::value;
+        const bool more = tile + gridDim.x < n_tiles;
+#ifndef IGR_GEMMP_NOLOAD
+        if (more) load((tile + gridDim.x) * TM, guard);
+#endif
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            f32x4 acc[NB][2];
+#pragma unroll
+            for (int j = 0; j < NB; ++j)
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb) acc[j][rb] = bz[j];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb) {
+                    const float a = As[buf][(16 * (2 * half + rb) + m16) * STR + 4 * ks + g];
+#pragma unroll
+                    for (int j = 0; j < NB; ++j)
+                        acc[j][rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[j][ks], a, acc[j][rb], 0, 0, 0);
+                }
+            }
+            if (half == 1 && more) stage(buf ^ 1);  // every wave left that buffer before the last barrier
+            // D map: column (= output row) lane & 15, rows (= output columns) 4 g + r
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                const int64_t gm = tile * TM + 16 * (2 * half + rb) + m16;
+#ifdef IGR_GEMMP_NOSTORE
+                if (gm < M && acc[0][rb][0] == 12345.678f) {
+#else
+                if (!GUARD || gm < M) {
+#endif
+#pragma unroll
+                    for (int j = 0; j < NB; ++j)
+                        *reinterpret_cast<f32x4 *>(C + gm * ldc + n0 + 16 * j + 4 * g) = acc[j][rb];
+                }
+            }
+        }
+        __syncthreads();
+        buf ^= 1;
+    };
+    // first the iterations whose tile and prefetched tile are both whole (the unguarded
+    // body, a loop of its own so that no guarded path joins it), then the last one or two
+    for (; tile + gridDim.x < full_tiles; tile += gridDim.x) body(std::false_type{});
+    for (; tile < n_tiles; tile += gridDim.x) body(std::true_type{});
+}
+
 // C[m, n] = bias[n] + sum_z W[z, m, n], z in order (deterministic split-K reduce)
 __global__ void splitk_reduce(int64_t M, int64_t N, int S, const float *__restrict__ W,
                               const float *__restrict__ bias, float *__restrict__ C, int64_t ldc) {
@@ -314,6 +445,40 @@ extern "C" int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int
 #ifndef IGR_GEMM128
 #define IGR_GEMM128 1
 #endif
+        // the register-resident-weight kernel: short K, N in whole 64-column groups
+        const bool rows_ok = !trans_a && S == 1 && (k == 32 || k == 64) && n % 64 == 0 && m >= 1024 &&
+                             lda % 4 == 0 && ldc % 4 == 0 && aligned16(a) && aligned16(c) && n / 64 <= 65535;
+        if (rows_ok) {
+            const int64_t tiles = (m + 63) / 64;
+            // wider column groups per workgroup once there are enough row tiles to fill the chip
+            const int nb = (n % 256 == 0 && tiles >= 512) ? 4 : ((n % 128 == 0 && tiles * 2 >= 512) ? 2 : 1);
+            static int cus = 0;
+            if (cus <= 0) {
+                int dev = 0;
+                if (hipGetDevice(&dev) != hipSuccess ||
+                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+                    cus = 256;
+            }
+            const int64_t gy = n / (64 * nb);
+            const int64_t gx = std::min<int64_t>(tiles, std::max<int64_t>(1, 2 * (int64_t)cus / gy));
+            dim3 gp((unsigned)gx, (unsigned)gy);
+#define IGR_GEMMP(KS_, NB_)                                                                                       \
+    do {                                                                                                          \
+        if (trans_b)                                                                                              \
+            hipLaunchKernelGGL((gemm_rows_persistent<KS_, NB_, true>), gp, dim3(256), 0, st, m, a, lda, b, ldb,   \
+                               bias, c, ldc);                                                                     \
+        else                                                                                                      \
+            hipLaunchKernelGGL((gemm_rows_persistent<KS_, NB_, false>), gp, dim3(256), 0, st, m, a, lda, b, ldb,  \
+                               bias, c, ldc);                                                                     \
+    } while (0)
+            if (k == 64) {
+                if (nb == 4) IGR_GEMMP(16, 4); else if (nb == 2) IGR_GEMMP(16, 2); else IGR_GEMMP(16, 1);
+            } else {
+                if (nb == 4) IGR_GEMMP(8, 4); else if (nb == 2) IGR_GEMMP(8, 2); else IGR_GEMMP(8, 1);
+            }
+#undef IGR_GEMMP
+            return launch_status(fn);
+        }
         // 128 tiles only when they still give >= 2048 workgroups (8 per CU): on
         // small shapes the 64 tiles' extra parallelism wins (measured)
         const int64_t tiles128 = ((m + BT - 1) / BT) * ((n + BT - 1) / BT);

@@ -10,13 +10,18 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, 'inductive-recommendation_amd')
 VARIANTS = {
-    'g64': '-DIGR_GEMM128=0',
+    # diagnostics of the persistent projection kernel: what it costs to store C / load A
+    'p_nostore': '-DIGR_GEMMP_NOSTORE',
+    'p_noload': '-DIGR_GEMMP_NOLOAD',
 }
+ONLY = os.environ.get('IGR_TUNE_SHAPES')
 # name: (m, n, k, trans_a, trans_b)
 SHAPES = {
     'att_fwd_ml1m': (9748, 256, 64, False, False), 'att_dx_ml1m': (9748, 64, 256, False, True),
     'att_dw_ml1m': (256, 64, 9748, True, True),
     'att_fwd_1m': (1_100_002, 256, 64, False, False), 'att_dw_1m': (256, 64, 1_100_002, True, True),
+    'ngcf_fwd_1m': (1_100_000, 64, 64, False, False), 'att_fwd_d32_1m': (1_100_002, 128, 32, False, False),
+    'att_fwd_11m': (11_000_002, 256, 64, False, False),
     'score_gowalla': (4096, 40981, 128, False, False), 'score_ml1m': (6040, 3706, 64, False, False),
 }
 
@@ -41,6 +46,8 @@ def one(name):
     dev = torch.device('cuda')
     res = {'variant': name}
     for sh, (m, n, k, ta, tb) in SHAPES.items():
+        if ONLY and sh not in ONLY.split(','):
+            continue
         a = torch.randn(*((k, m) if ta else (m, k)), device=dev)
         b = torch.randn(*((k, n) if tb else (n, k)), device=dev)
         for _ in range(3):

@@ -3,10 +3,13 @@
 Tolerance (fp32): |y - y64| <= 1e-5 |y64| + 1e-6 max|y64_row|
 against a float64 oracle; integer / index outputs bit-exact.
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
 
+from igr import _lib as L
 from igr import graph as G
 from igr import ops
 from oracle import igr_oracle as O
@@ -895,3 +898,25 @@ def test_gemm_128_tiles_every_transposition(m, n, k):
             b = B if tb else B.T.copy()
             c = ops.gemm(t(a), t(b), t(bias), trans_a=ta, trans_b=tb).cpu().numpy()
             close(c, ref, rtol=1e-5, atol_row=1e-5)
+
+
+@pytest.mark.parametrize('m,n,k,tb', [(4133, 256, 64, False), (1024, 64, 64, True), (33001, 256, 64, False),
+                                      (40000, 128, 32, False), (70000, 512, 64, True), (20011, 64, 32, False),
+                                      (17000, 128, 64, False), (1100002, 256, 64, False)])
+def test_gemm_register_resident_weight_kernel(m, n, k, tb):
+    """The persistent projection kernel (weight slice in registers, transposed MFMA,
+    direct 16-byte C stores): short K, N in 64-column groups, M tails, every
+    column-group width, bias as the accumulator's initial value, a strided A."""
+    rng = np.random.default_rng(m + n + k)
+    big = rng.standard_normal((m, k + 8)).astype(np.float32)
+    a = t(big)[:, 4:4 + k]  # leading dimension k + 8, 16-byte aligned offset
+    w = rng.standard_normal((k, n) if tb else (n, k)).astype(np.float32)
+    b = rng.standard_normal(n).astype(np.float32)
+    ref = big[:, 4:4 + k].astype(np.float64) @ (w if tb else w.T).astype(np.float64) + b
+    c = torch.full((m, n), float('nan'), device=DEV)
+    wd, bd = t(w), t(b)  # kept alive across the call
+    L.call('igr_gemm_f32', m, n, k, a.data_ptr(), a.stride(0), 0, wd.data_ptr(), w.shape[1], int(tb),
+           bd.data_ptr(), c.data_ptr(), n, None, 0, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    close(c.cpu().numpy(), ref, rtol=1e-5, atol_row=1e-5)
+    c2 = ops.gemm(t(np.ascontiguousarray(big[:, 4:4 + k])), wd, bd, trans_b=tb)
+    assert torch.equal(c, c2)  # the contiguous call takes the same kernel: same bits

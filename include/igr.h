@@ -293,6 +293,22 @@ int igr_dropout_uniforms(const igr_csr *g, uint64_t seed, uint64_t offset, const
 int igr_sddmm_dot_f32(const igr_csr *g, int32_t h, int32_t d, const float *u, int64_t ld_u,
                       const float *v, int64_t ld_v, float *out, void *stream);
 
+/* The attention SDDMM with one source row serving every head:
+ *   igr_sddmm_shared_f32:      out[eid(p), j] = <u[row_p, j, :], v[col_p, :]>
+ *   igr_spmm_shared_heads_f32: y[r, j, :] = sum_{p in row r} rhs[eid(p), j] * x[col_p, :]
+ *                              (the gradient of the former with respect to u)
+ * u, y: [n_rows, h*d]; v, x: [n_cols, d]; out, rhs: [nnz, h] by edge id.
+ * AttIGCN's score <x_q[r, j], W_k[j] E[c] + b_k[j]> (model.py:4246-4268) equals
+ * <W_k[j]^T x_q[r, j], E[c]> plus a term constant over the edges of row r, which the
+ * row softmax that follows (model.py:4270-4274) cancels: with W_k[j]^T folded into
+ * the query projection, every edge gathers the d floats of E[c] instead of the
+ * h*d floats of x_k[c], and x_k is never formed.  d in {32, 64, 128, 256}, h a
+ * power of two, h*d <= 512; 16-byte aligned operands. */
+int igr_sddmm_shared_f32(const igr_csr *g, int32_t h, int32_t d, const float *u, int64_t ld_u,
+                         const float *v, int64_t ld_v, float *out, void *stream);
+int igr_spmm_shared_heads_f32(const igr_csr *g, int32_t h, int32_t d, const float *x, int64_t ldx,
+                              const float *rhs, float *y, int64_t ldy, void *stream);
+
 /* gspmm(g, 'copy_rhs', 'sum'|'max', None, x): out[r, h] = reduce over edges
  * of row r of x[eid, h]; empty rows give 0 (model.py:4270, 4273).
  * reduce: 0 = sum, 1 = max. */

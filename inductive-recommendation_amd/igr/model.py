@@ -482,13 +482,39 @@ class AttIGCN(IGCN):
     def attention_values(self, feat_vals):
         """model.py:4258-4275.  After dropout the dropped edges are absent from
         the reference's graph; here they carry value 0 and are excluded from
-        the softmax through `keep`."""
+        the softmax through `keep`.
+
+        Default ('attention': 'folded'): the key projection is folded into the query
+        side.  <x_q[r, j], W_k[j] E[c] + b_k[j]> = <W_k[j]^T x_q[r, j], E[c]> + a term
+        constant over row r's edges, which the row softmax cancels exactly; and
+        W_k[j]^T (W_q[j] y + b_q[j]) is again one Linear(d, h d) of y = F E, with
+        weight M[j] = W_k[j]^T W_q[j] and bias W_k[j]^T b_q[j].  So x_k is never
+        formed (one projection GEMM instead of two), every edge gathers the d floats
+        of E[c] instead of the h d floats of x_k[c], and the backward has no
+        reverse-graph per-head SpMM (b_k's gradient is the exact zero the reference's
+        is up to rounding).  'attention': 'reference' keeps the reference's operation
+        order (x_k formed, per-head gathers)."""
         e = self.embedding.weight.detach()
-        x_k = ops.linear(e, self.weight_k)
-        x_q = ops.linear(ops.gspmm(self.feat_mat, 'mul', 'sum', e, feat_vals), self.weight_q)
-        alpha = ops.gsddmm(self.feat_mat, 'dot', x_q, x_k, h=self.n_heads)
+        y = ops.gspmm(self.feat_mat, 'mul', 'sum', e, feat_vals)
         keep = feat_vals if (self.training and self.dropout > 0) else None
+        H, d = self.n_heads, self.embedding_size
+        if self.config.get('attention', 'folded') == 'reference' or not self._foldable():
+            x_k = ops.linear(e, self.weight_k)
+            x_q = ops.linear(y, self.weight_q)
+            alpha = ops.gsddmm(self.feat_mat, 'dot', x_q, x_k, h=H)
+        else:
+            wq, wk = self.weight_q.weight.view(H, d, d), self.weight_k.weight.view(H, d, d)
+            m = torch.bmm(wk.transpose(1, 2), wq).reshape(H * d, d)                        # M[j] = W_k[j]^T W_q[j]
+            b = torch.bmm(wk.transpose(1, 2), self.weight_q.bias.view(H, d, 1)).reshape(H * d)
+            # b_k only shifts every edge of a row alike: no effect after the softmax, zero gradient
+            b = b + 0. * self.weight_k.bias.sum()
+            u = ops.Linear.apply(y, m, b)
+            alpha = ops.GSDDMMShared.apply(self.feat_mat, u, e, H)
         return ops.AttSoftmax.apply(self.feat_mat, alpha, ops.sqrt_scale(self.embedding_size), keep)
+
+    def _foldable(self):
+        d, H = self.embedding_size, self.n_heads
+        return d in (32, 64, 128, 256) and H in (1, 2, 4, 8) and H * d <= 512
 
     def inductive_rep_layer(self, feat_vals, return_alpha=False):
         w = self.attention_values(feat_vals)

@@ -263,6 +263,37 @@ def sddmm_dot(g: Graph, u, v, h=1, out=None):
     return out
 
 
+def sddmm_shared(g: Graph, u, v, h, out=None):
+    """out[eid, j] = <u[row, j, :], v[col, :]>: one source row of d floats serves all h heads
+    (igr_sddmm_shared_f32); u: [n_rows, h*d], v: [n_cols, d]."""
+    _dev(u, v, out)
+    u, ldu = _rows(u.reshape(u.shape[0], -1))
+    v, ldv = _rows(v)
+    d = v.shape[1]
+    if u.shape[0] < g.n_rows or v.shape[0] < g.n_cols or u.shape[1] != h * d:
+        raise IgrError(f'sddmm_shared shapes: u {tuple(u.shape)}, v {tuple(v.shape)}, h={h} for graph '
+                       f'{g.n_rows}x{g.n_cols}')
+    if out is None:
+        out = torch.empty(g.nnz, h, dtype=torch.float32, device=u.device)
+    L.call('igr_sddmm_shared_f32', ctypes.byref(g.csr), h, d, _p(u), ldu, _p(v), ldv, _p(out), _stream())
+    return out
+
+
+def spmm_shared_heads(g: Graph, x, rhs, h, out=None):
+    """out[r, j*d:(j+1)*d] = sum_{p in row r} rhs[eid(p), j] * x[col_p, :] (igr_spmm_shared_heads_f32)."""
+    _dev(x, rhs, out)
+    x, ldx = _rows(x)
+    d = x.shape[1]
+    rhs = _f32(rhs).contiguous()
+    if x.shape[0] < g.n_cols or rhs.numel() != g.nnz * h:
+        raise IgrError(f'spmm_shared_heads: x {tuple(x.shape)}, rhs {tuple(rhs.shape)} for {g.nnz} edges x {h} heads')
+    if out is None:
+        out = torch.empty(g.n_rows, h * d, dtype=torch.float32, device=x.device)
+    L.call('igr_spmm_shared_heads_f32', ctypes.byref(g.csr), h, d, _p(x), ldx, _p(rhs), _p(out), out.stride(0),
+           _stream())
+    return out
+
+
 def segment_reduce(g: Graph, x, reduce='sum'):
     _dev(x)
     x = _f32(x).contiguous()
@@ -466,6 +497,29 @@ class GSDDMMDot(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             dv = spmm_heads(g.reverse(), u, dout, h, out=torch.empty_like(v))
         return None, du, dv, None
+
+
+class GSDDMMShared(torch.autograd.Function):
+    """out[e, j] = <u[row_e, j], v[col_e]> with v shared by the heads; backward:
+    du[r, j] = sum_e dout[e, j] v[col_e] (one gather per edge for all heads).  v takes
+    no gradient here (AttIGCN detaches the embedding on this path, model.py:4258)."""
+
+    @staticmethod
+    def forward(ctx, g, u, v, h):
+        if v.requires_grad:
+            raise IgrError('gsddmm_shared: the shared source operand takes no gradient; detach it')
+        ctx.g, ctx.h = g, h
+        ctx.save_for_backward(v)
+        ctx.u_shape = u.shape
+        return sddmm_shared(g, u, v, h)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (v,) = ctx.saved_tensors
+        du = None
+        if ctx.needs_input_grad[1]:
+            du = spmm_shared_heads(ctx.g, v, dout.contiguous(), ctx.h).view(ctx.u_shape)
+        return None, du, None, None
 
 
 class SegmentSum(torch.autograd.Function):

@@ -67,6 +67,18 @@ def main():
     comp = g.nnz * (4 + 4 * H * d + 4 * H) + g.n_rows * 4 * H * d
     res['sddmm'] = {'ms': ms, 'edges_per_s': g.nnz / ms * 1e3, 'algorithmic_GBps': alg / ms / 1e6,
                     'frac': alg / ms / 1e6 / 8000.0, 'compulsory_GBps': comp / ms / 1e6}
+    # the folded form: one d-float source row per edge for all heads (igr_sddmm_shared_f32);
+    # algorithmic bytes per edge: col + eid-free out row + one 4d-byte source row
+    a2 = torch.empty_like(alpha)
+    ms = timed(lambda: ops.sddmm_shared(g, q, emb, H, out=a2), args.steps, args.warmup)
+    alg = g.nnz * (4 + 4 * d + 4 * H) + g.n_rows * (8 + 4 * H * d)
+    res['sddmm_shared'] = {'ms': ms, 'edges_per_s': g.nnz / ms * 1e3, 'algorithmic_GBps': alg / ms / 1e6,
+                           'frac': alg / ms / 1e6 / 8000.0}
+    du = torch.empty(g.n_rows, H * d, device=dev)
+    ms = timed(lambda: ops.spmm_shared_heads(g, emb, alpha, H, out=du), args.steps, args.warmup)
+    res['spmm_shared_heads_bwd'] = {'ms': ms, 'edges_per_s': g.nnz / ms * 1e3, 'algorithmic_GBps': alg / ms / 1e6,
+                                    'frac': alg / ms / 1e6 / 8000.0}
+    del a2, du
     ms = timed(lambda: ops.segment_reduce(g, alpha, 'max'), args.steps, args.warmup)
     byts = g.nnz * 4 * H + g.n_rows * (8 + 4 * H)
     res['segment_max'] = {'ms': ms, 'edges_per_s': g.nnz / ms * 1e3, 'algorithmic_GBps': byts / ms / 1e6,

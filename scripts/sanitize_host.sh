@@ -25,7 +25,7 @@ for san in address,undefined thread; do
       "./driver_$tag" ) 2>&1 | tee -a "$LOG"
 done
 echo "== hipcc, host pass with -fsanitize=address,undefined: whole library + Python host tests" | tee -a "$LOG"
-SRCS="spmm.hip spmm_rows.hip topk.hip edge_ops.hip bpr.hip rowsort.hip gemm.hip train_ops.hip graph_host.cpp capi.cpp"
+SRCS="spmm.hip spmm_rows.hip topk.hip edge_ops.hip att_shared.hip bpr.hip rowsort.hip gemm.hip train_ops.hip graph_host.cpp capi.cpp"
 OBJS=""
 for s in $SRCS; do
   o=$B/${s%.*}.o

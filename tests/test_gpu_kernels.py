@@ -920,3 +920,36 @@ def test_gemm_register_resident_weight_kernel(m, n, k, tb):
     close(c.cpu().numpy(), ref, rtol=1e-5, atol_row=1e-5)
     c2 = ops.gemm(t(np.ascontiguousarray(big[:, 4:4 + k])), wd, bd, trans_b=tb)
     assert torch.equal(c, c2)  # the contiguous call takes the same kernel: same bits
+
+
+@pytest.mark.parametrize('h,d,dedup', [(4, 64, True), (4, 64, False), (4, 32, True), (1, 64, True), (2, 128, False),
+                                       (8, 64, True), (2, 256, True), (8, 32, False), (1, 256, True)])
+def test_sddmm_shared_source_and_its_gradient(h, d, dedup):
+    """out[e, j] = <u[row_e, j], v[col_e]> (one source row for all heads) and
+    y[r, j] = sum_e rhs[e, j] v[col_e] against float64, multigraph edge ids included,
+    rows longer than a 64-edge block, empty rows; the gradient kernel is deterministic."""
+    g, _ = rand_graph(300, 200, 9000, seed=h * d, skew=True, dedup=dedup)
+    rng = np.random.default_rng(d + h)
+    u = rng.standard_normal((300, h * d)).astype(np.float32)
+    v = rng.standard_normal((200, d)).astype(np.float32)
+    hst = g.host()
+    row = np.repeat(np.arange(300), np.diff(hst['row_ptr']))
+    col = hst['col_idx'].astype(np.int64)
+    eid = hst['edge_id'] if hst['edge_id'] is not None else np.arange(g.nnz)
+    out = ops.sddmm_shared(g, t(u), t(v), h).cpu().numpy()
+    u64, v64 = u.astype(np.float64).reshape(300, h, d), v.astype(np.float64)
+    ref = np.empty((g.nnz, h))
+    ref[eid] = np.einsum('ehk,ek->eh', u64[row], v64[col])
+    mag = np.empty((g.nnz, h))
+    mag[eid] = np.einsum('ehk,ek->eh', np.abs(u64[row]), np.abs(v64[col]))
+    assert np.all(np.abs(out - ref) <= d * 2.0 ** -24 * mag + 1e-30)
+    rhs = rng.standard_normal((g.nnz, h)).astype(np.float32)
+    y = ops.spmm_shared_heads(g, t(v), t(rhs), h)
+    yr = np.zeros((300, h, d))
+    np.add.at(yr, row, rhs.astype(np.float64)[eid][:, :, None] * v64[col][:, None, :])
+    close(y.cpu().numpy(), yr.reshape(300, h * d), atol_row=2e-6)
+    assert torch.equal(y, ops.spmm_shared_heads(g, t(v), t(rhs), h))
+    # autograd: d/du of sum(out * rhs) is exactly that SpMM
+    ut = t(u).requires_grad_(True)
+    (ops.GSDDMMShared.apply(g, ut, t(v), h) * t(rhs)).sum().backward()
+    assert torch.equal(ut.grad, y)

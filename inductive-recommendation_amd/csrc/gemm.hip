@@ -267,23 +267,65 @@ __global__ __launch_bounds__(256) void gemm128_f32_mfma(int64_t M, int64_t N, in
 //  * the MFMA is issued transposed, D = W_slice (16 x 4) x A_tile^T (4 x 16), so a
 //    lane ends up with FOUR CONSECUTIVE COLUMNS of one output row: C leaves the
 //    registers as 16-byte stores with no LDS staging;
-//  * A tiles go global -> registers -> LDS (double-buffered, the next tile's loads
-//    issued before this tile's MFMAs and written to LDS after them, one barrier per
-//    tile), stride K + 4 floats so
-//    both the 16-byte staging stores and the operand reads are bank-conflict free;
+//  * A tiles go global -> registers -> LDS (double-buffered, the tile after next
+//    loaded while the next one is computed, one barrier per tile), stride K + 4
+//    floats so both the 16-byte staging stores and the operand reads are
+//    bank-conflict free;
+//  * a tile is computed as two halves of 32 rows with accumulator sets of their own,
+//    and the C stores of one half are spread through the MFMAs of the NEXT half (one
+//    16-byte store instruction per two k steps) instead of a burst of 2 NB stores
+//    after each half: a wave issues in order, so a burst holds its MFMAs back for as
+//    long as the store queue takes to accept it, on all four SIMDs at once;
+//  * the only wait on memory is the one before the next tile goes to LDS; memory
+//    operations retire in order and those loads are older than the stores that
+//    follow them, so C drains under the MFMAs;
 //  * bias is the accumulators' initial value.
-// Two workgroups per CU: one wave's loads / stores overlap the other's MFMAs.
+// Rows past M are never stored; loads clamp the row index, so every tile is read
+// with straight-line code.  Two workgroups per CU.
+// A tile of TM rows x K floats: global -> registers (row index clamped to M - 1, so the
+// code is straight-line for every tile) and registers -> LDS image with row stride K + 4.
+template <int K, int LP>
+__device__ __forceinline__ void rows_tile_load(f32x4 (&ra)[LP], const float *__restrict__ A, int64_t lda, int64_t M,
+                                               int64_t m0, int t) {
+#pragma unroll
+    for (int i = 0; i < LP; ++i) {
+        const int idx = t + i * 256;
+        int64_t gm = m0 + idx / (K / 4);
+        gm = gm < M ? gm : M - 1;
+        ra[i] = *reinterpret_cast<const f32x4 *>(A + gm * lda + (idx % (K / 4)) * 4);
+    }
+}
+template <int K, int LP>
+__device__ __forceinline__ void rows_tile_stage(const f32x4 (&ra)[LP], float *as, int t) {
+#pragma unroll
+    for (int i = 0; i < LP; ++i) {
+        const int idx = t + i * 256;
+        *reinterpret_cast<f32x4 *>(as + (idx / (K / 4)) * (K + 4) + (idx % (K / 4)) * 4) = ra[i];
+    }
+}
+
+#ifndef IGR_GEMMP_OCC
+#define IGR_GEMMP_OCC 2
+#endif
+#ifndef IGR_GEMMP_PIN
+#define IGR_GEMMP_PIN 0x106
+#endif
 template <int KS, int NB, bool TB>
-__global__ __launch_bounds__(256, 2) void gemm_rows_persistent(int64_t M, const float *__restrict__ A, int64_t lda,
-                                                              const float *__restrict__ B, int64_t ldb,
-                                                              const float *__restrict__ bias,
-                                                              float *__restrict__ C, int64_t ldc) {
+__global__ __launch_bounds__(256, IGR_GEMMP_OCC) void gemm_rows_persistent(int64_t M, const float *__restrict__ A,
+                                                                         int64_t lda, const float *__restrict__ B,
+                                                                         int64_t ldb, const float *__restrict__ bias,
+                                                                         float *__restrict__ C, int64_t ldc) {
     constexpr int K = KS * 4, TM = 64, STR = K + 4;
-    constexpr int LP = TM * K / 4 / 256;  // float4 per thread per A tile
+    constexpr int LP = TM * K / 4 / 256;
+    constexpr int NST = 2 * NB;          // store instructions per half
+    constexpr int GAP = KS / NST > 0 ? KS / NST : 1;  // k steps between two of them
     __shared__ __align__(16) float As[2][TM * STR];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int m16 = lane & 15, g = lane >> 4;
     const int64_t n0 = (int64_t)blockIdx.y * (64 * NB) + wave * (16 * NB);
+    const int64_t n_tiles = (M + TM - 1) / TM, full_tiles = M / TM;
+    int64_t tile = blockIdx.x;
+    if (tile >= n_tiles) return;  // the whole workgroup leaves together, before any barrier
     float w[NB][KS];
     f32x4 bz[NB];
 #pragma unroll
@@ -297,91 +339,74 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_persistent(int64_t M, const 
 #pragma unroll
         for (int r = 0; r < 4; ++r) bz[j][r] = bias ? bias[n0 + 16 * j + 4 * g + r] : 0.f;
     }
-    float4 ra[LP];
-    // GUARD = false: the tile lies wholly inside M - straight-line code, so the
-    // compiler can count the memory operations in flight exactly
-    auto load = [&](int64_t m0, auto guard) {
-#pragma unroll
-        for (int i = 0; i < LP; ++i) {
-            const int idx = t + i * 256;
-            const int64_t gm = m0 + idx / (K / 4);
-            if (!decltype(guard)::value || gm < M)
-                ra[i] = *reinterpret_cast<const float4 *>(A + gm * lda + (idx % (K / 4)) * 4);
-            else
-                ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    };
-    auto stage = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < LP; ++i) {
-            const int idx = t + i * 256;
-            *reinterpret_cast<float4 *>(&As[buf][(idx / (K / 4)) * STR + (idx % (K / 4)) * 4]) = ra[i];
-        }
-    };
-    const int64_t n_tiles = (M + TM - 1) / TM, full_tiles = M / TM;
-    int64_t tile = blockIdx.x;
-    if (tile < n_tiles) {
-        load(tile * TM, std::true_type{});
-        stage(0);
-    }
-    // Every load above (the weight slice, the bias) completes HERE.  Left to the first
-    // use inside the loop, the wait would sit in the loop body and, counting memory
-    // operations in order, would there also cover the A loads and C stores of every
-    // iteration: no overlap at all.
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    int buf = 0;
-    // A tile is computed as two halves of 32 rows, each with its own accumulators, in
-    // the order: next tile's loads, half 0, stores 0, half 1, next tile into the other
-    // LDS buffer, stores 1, barrier.  The only wait on memory is the one before the
-    // next tile goes to LDS; memory operations retire in order and the loads are older
-    // than stores 0, so it leaves those stores in flight: C drains under the MFMAs.
-    auto body = [&](auto guard) {
-        constexpr bool GUARD = decltype(guard)::value;
-        const bool more = tile + gridDim.x < n_tiles;
-#ifndef IGR_GEMMP_NOLOAD
-        if (more) load((tile + gridDim.x) * TM, guard);
+    f32x4 ra[LP];  // a native vector: a struct float4 would be copied with memcpy and stay in scratch
+    auto load = [&](int64_t m0) __attribute__((always_inline)) { rows_tile_load<K, LP>(ra, A, lda, M, m0, t); };
+    auto stage = [&](int b) __attribute__((always_inline)) { rows_tile_stage<K, LP>(ra, As[b], t); };
+    // one store instruction: columns 16 j + 4 g .. + 3 of row m0 + 16 rb + m16
+    auto store1 = [&](const f32x4 (&src)[NB][2], int64_t m0, int s, auto guard) __attribute__((always_inline)) {
+        const int rb = s / NB, j = s % NB;
+        const int64_t gm = m0 + 16 * rb + m16;
+#ifdef IGR_GEMMP_NOSTORE
+        if (gm < M && src[0][rb][0] == 12345.678f)
+#else
+        if (!decltype(guard)::value || gm < M)
 #endif
+            *reinterpret_cast<f32x4 *>(C + gm * ldc + n0 + 16 * j + 4 * g) = src[j][rb];
+    };
+    // MFMAs of rows [32 half, 32 half + 32) of the tile in As[buf] into dst; when STORE, the
+    // 2 NB stores of `src` (rows m0 ...) are issued one every GAP k steps on the way
+    auto half_pass = [&](int buf, int half, f32x4 (&dst)[NB][2], const f32x4 (&src)[NB][2], int64_t m0,
+                         auto do_store, auto guard) __attribute__((always_inline)) {
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            f32x4 acc[NB][2];
+        for (int j = 0; j < NB; ++j)
 #pragma unroll
-            for (int j = 0; j < NB; ++j)
+            for (int rb = 0; rb < 2; ++rb) dst[j][rb] = bz[j];
 #pragma unroll
-                for (int rb = 0; rb < 2; ++rb) acc[j][rb] = bz[j];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-                for (int rb = 0; rb < 2; ++rb) {
-                    const float a = As[buf][(16 * (2 * half + rb) + m16) * STR + 4 * ks + g];
-#pragma unroll
-                    for (int j = 0; j < NB; ++j)
-                        acc[j][rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[j][ks], a, acc[j][rb], 0, 0, 0);
-                }
-            }
-            if (half == 1 && more) stage(buf ^ 1);  // every wave left that buffer before the last barrier
-            // D map: column (= output row) lane & 15, rows (= output columns) 4 g + r
+        for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb) {
-                const int64_t gm = tile * TM + 16 * (2 * half + rb) + m16;
-#ifdef IGR_GEMMP_NOSTORE
-                if (gm < M && acc[0][rb][0] == 12345.678f) {
-#else
-                if (!GUARD || gm < M) {
-#endif
+                const float a = As[buf][(16 * (2 * half + rb) + m16) * STR + 4 * ks + g];
 #pragma unroll
-                    for (int j = 0; j < NB; ++j)
-                        *reinterpret_cast<f32x4 *>(C + gm * ldc + n0 + 16 * j + 4 * g) = acc[j][rb];
-                }
+                for (int j = 0; j < NB; ++j)
+                    dst[j][rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[j][ks], a, dst[j][rb], 0, 0, 0);
+            }
+            if (decltype(do_store)::value && ks % GAP == GAP - 1 && ks / GAP < NST) {
+                store1(src, m0, ks / GAP, guard);
+                // keep the store where it stands: without this the scheduler gathers the
+                // stores of a half back into one burst.  LDS reads, VALU and SALU may cross.
+                __builtin_amdgcn_sched_barrier(IGR_GEMMP_PIN);
             }
         }
+        if (decltype(do_store)::value)
+#pragma unroll
+            for (int s = KS / GAP; s < NST; ++s) store1(src, m0, s, guard);
+    };
+    f32x4 acc0[NB][2], acc1[NB][2];
+    load(tile * TM);
+    stage(0);
+    // the weight slice, the bias and the first tile are complete here: no wait inside
+    // the loop ever has to count them
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    load((tile + gridDim.x) * TM);
+    half_pass(0, 0, acc0, acc1, 0, std::false_type{}, std::false_type{});
+    int buf = 0;
+    auto step = [&](auto guard) __attribute__((always_inline)) {
+        // half 1 of this tile while half 0 leaves
+        half_pass(buf, 1, acc1, acc0, tile * TM, std::true_type{}, guard);
+        stage(buf ^ 1);  // the next tile; every wave left that buffer before the last barrier
         __syncthreads();
+        load((tile + 2 * gridDim.x) * TM);
+        // half 0 of the next tile while half 1 of this one leaves
+        half_pass(buf ^ 1, 0, acc0, acc1, tile * TM + 32, std::true_type{}, guard);
         buf ^= 1;
     };
-    // first the iterations whose tile and prefetched tile are both whole (the unguarded
-    // body, a loop of its own so that no guarded path joins it), then the last one or two
-    for (; tile + gridDim.x < full_tiles; tile += gridDim.x) body(std::false_type{});
-    for (; tile < n_tiles; tile += gridDim.x) body(std::true_type{});
+    for (; tile + gridDim.x < full_tiles; tile += gridDim.x) step(std::false_type{});
+    for (; tile + gridDim.x < n_tiles; tile += gridDim.x) step(std::true_type{});
+    // the last tile of this workgroup
+    half_pass(buf, 1, acc1, acc0, tile * TM, std::true_type{}, std::true_type{});
+#pragma unroll
+    for (int s = 0; s < NST; ++s) store1(acc1, tile * TM + 32, s, std::true_type{});
 }
 
 // C[m, n] = bias[n] + sum_z W[z, m, n], z in order (deterministic split-K reduce)
@@ -460,7 +485,7 @@ extern "C" int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int
                     cus = 256;
             }
             const int64_t gy = n / (64 * nb);
-            const int64_t gx = std::min<int64_t>(tiles, std::max<int64_t>(1, 2 * (int64_t)cus / gy));
+            const int64_t gx = std::min<int64_t>(tiles, std::max<int64_t>(1, IGR_GEMMP_OCC * (int64_t)cus / gy));
             dim3 gp((unsigned)gx, (unsigned)gy);
 #define IGR_GEMMP(KS_, NB_)                                                                                       \
     do {                                                                                                          \

@@ -10,9 +10,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, 'inductive-recommendation_amd')
 VARIANTS = {
-    # diagnostics of the persistent projection kernel: what it costs to store C / load A
+    # the store placement of the persistent projection kernel
+    'p_pin0': '-DIGR_GEMMP_PIN=0',                          # nothing may cross a store
+    # diagnostics: what it costs to store C / load A
     'p_nostore': '-DIGR_GEMMP_NOSTORE',
-    'p_noload': '-DIGR_GEMMP_NOLOAD',
 }
 ONLY = os.environ.get('IGR_TUNE_SHAPES')
 # name: (m, n, k, trans_a, trans_b)
@@ -50,19 +51,27 @@ def one(name):
             continue
         a = torch.randn(*((k, m) if ta else (m, k)), device=dev)
         b = torch.randn(*((k, n) if tb else (n, k)), device=dev)
+        # The first ~50 launches after an idle GPU run 10-30 % slower than the sustained rate
+        # (clock / power management settling; scripts/gemm_clock_probe.py), so: `cold_us` = median
+        # of the first 20 launches after 3, `us` = median of 50 launches after >= 150 ms of them.
+        def timed(cnt):
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(cnt)]
+            for e0, e1 in ev:
+                e0.record()
+                ops.gemm(a, b, trans_a=ta, trans_b=tb)
+                e1.record()
+            torch.cuda.synchronize()
+            return [e0.elapsed_time(e1) * 1e3 for e0, e1 in ev]
         for _ in range(3):
             c = ops.gemm(a, b, trans_a=ta, trans_b=tb)
         torch.cuda.synchronize()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
-        for e0, e1 in ev:
-            e0.record()
-            ops.gemm(a, b, trans_a=ta, trans_b=tb)
-            e1.record()
-        torch.cuda.synchronize()
-        us = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev])) * 1e3
+        cold = timed(20)
+        n_warm = int(min(2000, max(20, 150e3 / max(float(np.median(cold)), 1.0))))
+        timed(n_warm)
+        us = float(np.median(timed(50)))
         ref = (a.t() if ta else a).double() @ (b if tb else b.t()).double()
         err = float(((c.double() - ref).abs().max() / ref.abs().max()).item())
-        res[sh] = {'us': us, 'tflops': 2 * m * n * k / us / 1e6, 'max_rel_err': err}
+        res[sh] = {'us': us, 'cold_us': float(np.median(cold)), 'tflops': 2 * m * n * k / us / 1e6, 'max_rel_err': err}
         del a, b, c, ref
         torch.cuda.empty_cache()
     print(json.dumps(res), flush=True)

@@ -40,13 +40,13 @@ def log(*a):
 
 
 def spmm_bytes(nnz, n_rows, d):
-    """Algorithmic bytes of one SpMM launch (SURVEY.md §8d): int32 col + fp32 val
+    """Algorithmic bytes of one SpMM launch: int32 col + fp32 val
     + one gathered fp32 source row per edge; int64 row_ptr + one output row per row."""
     return nnz * (4 + 4 + 4 * d) + n_rows * (8 + 4 * d)
 
 
 def compulsory_bytes(nnz, n_rows, n_src, d):
-    """SURVEY.md §8d's informational lower bound: the CSR once, every source row
+    """Informational lower bound: the CSR once, every source row
     once and every output row once (perfect cache reuse of the gathers)."""
     return nnz * 8 + n_rows * (8 + 4 * d) + n_src * 4 * d
 

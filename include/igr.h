@@ -1,15 +1,15 @@
 /*
  * igr.h - C-ABI of the MI355X (gfx950) inductive graph-convolution path.
  *
- * Drop-in boundary for the DGL operator API the reference sits on
- * (SURVEY.md §8b).  The reference binds, from Python:
+ * Drop-in boundary for the DGL operator API the reference sits on.
+ * The reference binds, from Python:
  *     g = dgl.graph((column, row), num_nodes=n, device=dev)      model.py:103-105, 4183, 4194
  *     dgl.ops.gspmm(g, 'mul', 'sum', lhs_data=X, rhs_data=vals)  model.py:106, 4184, 4196, 4037
  *     dgl.ops.gspmm(g, 'copy_rhs', 'max'|'sum', None, alpha)     model.py:4270, 4273 (AttIGCN)
  *     AttIGCN.masked_mm (index_select x2 + mul + sum)             model.py:4246-4255
  *     rep[users], rep[n_users + pos/neg] (BPR gathers)            model.py:4048-4049
  * Every entry point below replaces one of those; the ctypes binding that
- * calls them is inductive-recommendation_amd/igr/_lib.py (INTEGRATION.md).
+ * calls them is inductive-recommendation_amd/igr/_lib.py.
  *
  * Conventions
  *  - Plain pointers and sizes.  Device pointers are HIP device memory
@@ -75,7 +75,7 @@ typedef struct igr_csr {
  * lets the backward pre-scale dx_0 by the feature graph's row scale, so the
  * transposed feature SpMM gathers no per-edge column scale.  row_mask /
  * col_mask restrict a layer to the rows a training step's loss can reach
- * and its backward to the source rows that carry gradient (DESIGN.md §8b). */
+ * and its backward to the source rows that carry gradient. */
 typedef struct igr_epilogue {
     float alpha;
     float beta;
@@ -114,7 +114,7 @@ int igr_csr_from_coo(int64_t n_rows, int64_t n_cols, int64_t nnz, const int64_t 
                      int32_t *col_idx, float *val_out, int64_t *edge_id, int64_t *nnz_out,
                      int32_t n_threads);
 
-/* Transposed CSR (reverse graph for the gspmm backward):
+/* Transposed CSR (reverse graph for the gspmm backward, model.py:106, 4196):
  * t_row_ptr [n_cols+1], t_col_idx [nnz] (= source row), t_pos [nnz] = CSR
  * position in the forward graph of each transposed entry. */
 int igr_csr_transpose(int64_t n_rows, int64_t n_cols, const int64_t *row_ptr,
@@ -391,7 +391,7 @@ int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int64_t lda, i
 
 /* ------------------------------------------------------- training step */
 
-/* Device-side BPR sampler (dataset.py:119-131 semantics, SURVEY §8f row 1):
+/* Device-side BPR sampler (dataset.py:119-131 semantics):
  * for each b < batch: users[b] = active[uniform], pos[b] = uniform item of that
  * user's sorted training list items[row_ptr[u] .. row_ptr[u+1]), neg[b] =
  * uniform item not in that list (rejection, at most max_rounds redraws).
@@ -404,7 +404,7 @@ int igr_bpr_sample(int64_t batch, int64_t n_active, const int32_t *active, const
                    void *stream);
 
 /* Fused Adam step (torch.optim.Adam semantics, amsgrad off; trainer.py:44-46,
- * 555; SURVEY §8f row 3): one pass over p, g, m, v.  `step` is the 1-based
+ * 555): one pass over p, g, m, v.  `step` is the 1-based
  * step count after increment (bias corrections).  step_dev (nullable, device
  * int64): the step is step + *step_dev and the bias corrections are formed on
  * the device (hipGraph-captured steps). */

@@ -505,7 +505,7 @@ extern "C" int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int
             return launch_status(fn);
         }
         // 128 tiles only when they still give >= 2048 workgroups (8 per CU): on
-        // small shapes the 64 tiles' extra parallelism wins (measured, DESIGN.md §3)
+        // small shapes the 64 tiles' extra parallelism wins (measured)
         const int64_t tiles128 = ((m + BT - 1) / BT) * ((n + BT - 1) / BT);
         if (IGR_GEMM128 && S == 1 && tiles128 >= 2048 && (n + BT - 1) / BT <= 65535) {
             dim3 g2((unsigned)((m + BT - 1) / BT), (unsigned)((n + BT - 1) / BT));

@@ -1,10 +1,10 @@
 // spmm.hip - CSR SpMM (DGL gspmm 'mul'/'sum') for gfx950.
 //
 // Replaces dgl.ops.gspmm(g, 'mul', 'sum', lhs, rhs) at model.py:106, 4184,
-// 4196, 4037 and its reverse-graph backward (SURVEY.md §8a A7-A9):
+// 4196, 4037 and its reverse-graph backward:
 //     y[r] = sum_{p in row r} rhs[eid(p)] * x[col[p]]          (fp32)
 //
-// Design (DESIGN.md §3):
+// Design:
 //  * One feature row of x is D fp32 = D/4 float4; LPR = D/4 lanes cover it
 //    with one 16-B load each, so a wave64 holds G = 64/LPR rows.
 //  * Row tier: each LPR-lane group owns one output row.  Rows are visited in
@@ -643,7 +643,7 @@ extern "C" int igr_spmm_heads_f32(const igr_csr *g, int32_t h, int32_t d, const 
         if (g->nnz > 0 && !rhs) return arg_error(fn, "rhs is NULL");
         if (ldx < (int64_t)h * d || ldy < (int64_t)h * d) return arg_error(fn, "leading dimension < h*d");
         // one launch per head: each gathers only its d-column slice of x (the
-        // slices of a small table stay L2-resident, DESIGN.md §3)
+        // slices of a small table stay L2-resident)
         for (int32_t j = 0; j < h; ++j) {
             const int rc = run_spmm(fn, g, d, x ? x + (int64_t)j * d : nullptr, ldx,
                                     W_ValHead{rhs, g->edge_id, h, j}, y ? y + (int64_t)j * d : nullptr, ldy,

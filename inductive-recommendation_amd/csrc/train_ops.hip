@@ -2,9 +2,9 @@
 //
 //   igr_bpr_sample          device-side BPR negative sampler      dataset.py:119-131
 //                           (replaces the CPU sampler in 6 DataLoader workers + H2D,
-//                            trainer.py:522-535; SURVEY.md §8f row 1)
+//                            trainer.py:522-535)
 //   igr_adam_f32            fused Adam update, torch.optim.Adam    trainer.py:44-46, 555
-//                           semantics in one pass (SURVEY.md §8f row 3)
+//                           semantics in one pass
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>

@@ -1,7 +1,7 @@
 """ctypes binding of the igr C ABI (include/igr.h) -> lib/libigr.so.
 
 This is the reference-side binding a maintainer adds next to the DGL call
-sites (INTEGRATION.md): plain pointers, sizes and a hipStream_t; no torch
+sites: plain pointers, sizes and a hipStream_t; no torch
 types cross the boundary.  Loading fails loudly if the library is missing -
 there is no CPU fallback for the device entry points.
 """

@@ -1,7 +1,7 @@
 """igr.config - the in-scope rows of the reference's config tables.
 
 Same (dataset_config, model_config, trainer_config) dict triples as
-config.py:1-527, restricted to the models of the hot path (SURVEY.md §2 #12):
+config.py:1-527, restricted to the models of the hot path:
 LightGCN / IGCN / IMF / NGCF on ML-1M (config.py:400-470) and Gowalla
 (config.py:1-40), plus the synthetic benchmark graphs of BASELINE.json.
 """

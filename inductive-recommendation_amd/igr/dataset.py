@@ -6,8 +6,7 @@ sampler (dataset.py:119-131).  BPRBatchSampler draws whole batches with the
 same distribution in vectorised numpy (the reference runs the per-sample
 Python sampler in 6 DataLoader workers, trainer.py:522-526).
 SyntheticDataset builds the benchmark's random bipartite graphs;
-GowallaDataset / YelpDataset / AmazonDataset / MovieLensDataset ingest raw logs
-(SURVEY.md §8f row 4).
+GowallaDataset / YelpDataset / AmazonDataset / MovieLensDataset ingest raw logs.
 """
 import os
 import random
@@ -87,7 +86,7 @@ def read_split(file_path):
 
 
 def ingest(raw_users, raw_items, times, min_inter, split_ratio):
-    """Vectorised restatement of the reference's raw pipeline (SURVEY.md §8f row 4):
+    """Vectorised restatement of the reference's raw pipeline:
       remove_sparse_ui (dataset.py:66-92): iterative k-core on unique (user, item)
         pairs - users with < min_inter items removed, then items with < min_inter
         users, repeated until stable; survivors numbered in first-appearance order;
@@ -277,7 +276,7 @@ class AuxiliaryDataset(BasicDataset):
 
 
 class SyntheticDataset(BasicDataset):
-    """Random bipartite interactions (BASELINE.md §3): users ~ U[0, n_users),
+    """Random bipartite interactions: users ~ U[0, n_users),
     items ~ U[0, n_items) or Zipf(s) ; duplicates kept in train_array and
     summed by the graph build exactly as utils.generate_daj_mat does.
     val/test hold `n_eval` random items per user (synthetic; metrics are not

@@ -1,7 +1,7 @@
 """igr.dist - edge-range sharded bipartite propagation across the GPUs of a node.
 
-The reference has no parallelism; this is the build's
-own multi-GPU layer.  Partition:
+The reference has no parallelism; this is the build's own multi-GPU layer.
+Partition:
 
   * users are cut into `world` contiguous ranges with balanced edge counts;
     rank k owns user rows U_k, every edge of those users (both directions)
@@ -34,7 +34,7 @@ MALL_BYTES = 256 << 20  # MI355X Infinity Cache
 
 def sharded_side(n_users, n_items, replicate='auto'):
     """'users' or 'items': the side a BipartiteShard cuts into ranges (the other is
-    replicated); 'auto' replicates the smaller side (SURVEY §8e)."""
+    replicated); 'auto' replicates the smaller side."""
     if replicate == 'auto':
         return 'users' if n_users >= n_items else 'items'
     if replicate not in ('items', 'users'):
@@ -175,7 +175,7 @@ class BipartiteShard:
         masks = (mode, user_bits, item_bits), bitmaps over local users / items:
         mode 'row' computes only the marked output rows (the others are left
         as they were), mode 'col' reads only the marked source rows (the others
-        must hold zeros) - dist_train's batch-row step (DESIGN.md §8b).
+        must hold zeros) - dist_train's batch-row step.
         `spmm(g, x, vals, out, accumulate, add=None, beta=0., row_mask=None,
         col_mask=None)` defaults to the HIP kernel (the CPU gloo tests pass the
         oracle); `hook(i, 'start'|'end')` brackets each SpMM launch (bench timing).
@@ -222,7 +222,7 @@ class BipartiteShard:
         hook(i, 'start')
         # wide rows whose item table outgrows the Infinity Cache (d = 256 at 1M
         # items): two passes over 128-column halves, each gathering from a
-        # cache-sized slice (same sums, column by column; DESIGN.md §3)
+        # cache-sized slice (same sums, column by column)
         d = x_items.shape[1]
         W = _col_width(d, x_items.shape[0] * d * 4)
         for c in range(0, d, W):

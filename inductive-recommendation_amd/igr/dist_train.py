@@ -1,4 +1,4 @@
-"""igr.dist_train - IGCN training sharded across the GPUs of a node ("Training").
+"""igr.dist_train - IGCN training sharded across the GPUs of a node.
 
 The reference trains on one device (trainer.py:518-561); this is the build's
 data-parallel restatement of the same step over the partition of igr.dist:

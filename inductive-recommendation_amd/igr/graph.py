@@ -5,7 +5,7 @@ of the reference (model.py:103-105, 4183, 4194): the structure is built once
 on the host (C++ in libigr, include/igr.h) and kept on the device; only edge
 values change between steps (dropout, anneal).
 
-Layout in HBM (DESIGN.md §2):
+Layout in HBM:
     row_ptr  int64[n_rows+1]   col_idx int32[nnz]   edge_id int64[nnz] | None
     order    int32[n_order]    rows of degree <= split_threshold, heaviest first
     split_row int32, split_ptr int64, chunk_row int32, chunk_beg int64  (long rows)

@@ -6,7 +6,7 @@ and autograd bookkeeping; every hot-path byte is moved by the HIP kernels.
 Ops raise IgrError for tensors that are not on a ROCm device (no CPU
 fallback).
 
-DGL-compatible surface (the reference's operator API, SURVEY.md §8b):
+DGL-compatible surface (the reference's operator API):
     graph((src, dst), num_nodes, device)       ~ dgl.graph       model.py:103-105
     gspmm(g, 'mul', 'sum', lhs, rhs)           ~ dgl.ops.gspmm   model.py:106, 4184, 4196, 4037
     gspmm(g, 'copy_rhs', 'sum'|'max', None, e) ~ dgl.ops.gspmm   model.py:4270, 4273

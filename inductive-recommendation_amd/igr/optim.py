@@ -3,7 +3,7 @@
 Drop-in for the `Adam` the reference resolves by name (trainer.py:44-46):
 same constructor (params, lr, betas, eps, weight_decay) and torch.optim.Adam
 update rule, one pass over (param, grad, exp_avg, exp_avg_sq) per tensor
-instead of torch's multi-kernel foreach sequence (SURVEY.md §8f row 3).
+instead of torch's multi-kernel foreach sequence.
 """
 import ctypes
 

@@ -5,7 +5,7 @@ uniform over users with training items, a positive uniform over that user's
 items, a negative uniform over items not in the user's training list.  The
 training lists live in HBM as a CSR; each batch is one kernel launch with a
 counter-based RNG keyed by (seed, step), so nothing crosses PCIe per step
-(SURVEY.md §8f row 1: the reference samples on the CPU in 6 DataLoader
+(the reference samples on the CPU in 6 DataLoader
 workers and copies every batch host->device, trainer.py:522-535).
 """
 import ctypes

@@ -207,7 +207,7 @@ def igcn_rep(A, F, fvals, emb, n_layers):
 
 
 def igcn_grad(A, F, fvals, n_layers, g):
-    """d/dEmb of sum(igcn_rep * G): gspmm backward = reverse-graph SpMM."""
+    """d/dEmb of sum(igcn_rep * G): gspmm backward = reverse-graph SpMM (model.py:106, 4196)."""
     L1 = n_layers + 1
     dx = (g / np.float32(L1)).astype(np.float32)
     for _ in range(n_layers):

@@ -1,4 +1,4 @@
-"""The attention inductive layer's edge kernels at scale (A10 / A11).
+"""The attention inductive layer's edge kernels at scale (model.py:4246-4275).
 
 IGCN's feature graph over the synthetic bipartite graph (feature_ratio 1,
 nnz_F = 2E + N, igr.dist_train.FeatureShard at world 1), H = 4 heads of d:
@@ -6,7 +6,7 @@ nnz_F = 2E + N, igr.dist_train.FeatureShard at world 1), H = 4 heads of d:
   softmax    per-row max-shifted exp / sum, head mean            (igr_att_softmax_f32)
   segment    gspmm copy_rhs max over alpha (the DGL-surface op)   (igr_segment_reduce_f32)
   spmm       out = SpMM(E, w) with the per-edge attention values (igr_spmm_f32)
-HIP events per launch.  SDDMM algorithmic bytes per SURVEY §8d:
+HIP events per launch.  SDDMM algorithmic bytes:
 nnz (8 + 2*4*H*d) + nnz * 4H (q row and k row per edge, no cache credit; the
 kernel keeps a row's q in registers, so its compulsory bytes are
 nnz (4 + 4*H*d + 4H) + rows * 4*H*d).  Softmax: 3 passes over the H scalars

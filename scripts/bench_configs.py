@@ -6,7 +6,7 @@ the symmetric D^-1/2 A D^-1/2 adjacency built exactly as
 utils.generate_daj_mat + LightGCN.generate_graph (igr.model.build_norm_adj),
 and
   * one SpMM Y = A X over the whole N x N adjacency (HIP events, median of 20
-    launches after 3 warm-ups), with SURVEY §8d's algorithmic bytes
+    launches after 3 warm-ups), with the algorithmic bytes
     nnz*(8 + 4d) + n*(8 + 4d) and their fraction of the 8 TB/s HBM peak.  Below
     ~100 MB of working set the tables live in L2 / Infinity Cache, so the
     fraction can exceed 1 there: it is not an HBM number at those sizes;

@@ -1,4 +1,4 @@
-"""The inductive layer's SpMM (A7 / A9, SURVEY §8d: timed separately from the adjacency).
+"""The inductive layer's SpMM (model.py:4184, 4189; timed separately from the adjacency).
 
 IGCN's feature graph at feature_ratio = 1 over the synthetic bipartite graph
 (rows [users; items], columns [user features; item features; 2 generals],

@@ -1,4 +1,4 @@
-"""IGCN training-step throughput on one GPU (reported in DESIGN.md, not the bench metric).
+"""IGCN training-step throughput on one GPU (not the bench metric).
 
 One step = IGCNTrainer.step: device BPR sampling (main + aux batch), dropout
 of the feature values, inductive SpMM + L LightGCN SpMMs (fused layer mean),

@@ -8,7 +8,7 @@ How the reference is run
 ------------------------
 `/root/reference/{utils,dataset,model,trainer}.py` are imported as-is.  Three
 third-party modules they import at top level are absent from the image and
-are registered in `sys.modules` before the import (SURVEY.md §8c):
+are registered in `sys.modules` before the import:
 
 * `dgl` (DGL >= 0.8, README.md:8, no pinned version).  Only `dgl.graph` and
   `dgl.ops.gspmm` are reached on the hot path.  `gspmm` is restated from DGL's
@@ -27,7 +27,7 @@ restated semantics above plus a float64 scipy cross-check.
 
 AttIGCN (model.py:4223-4287) is dead code inside a string literal; this
 script evaluates that class text against the imported `model` module
-namespace so its forward can be pinned too (SURVEY.md §3.5).
+namespace so its forward can be pinned too.
 
 Run:  python tests/golden/make_golden.py
 """
@@ -174,7 +174,7 @@ def main():
         ds = ToyDataset(nu, ni, edges, name=cname)
         fx = {'n_users': np.int64(nu), 'n_items': np.int64(ni), 'train_array': edges.astype(np.int64)}
 
-        # --- A1/A2/A3: adjacency, degree, sym-normalised values (utils.py:42-50, model.py:89-98)
+        # --- adjacency, degree, sym-normalised values (utils.py:42-50, model.py:89-98)
         adj = ref_utils.generate_daj_mat(ds)
         fx['adj_indptr'] = adj.indptr.astype(np.int64)
         fx['adj_indices'] = adj.indices.astype(np.int64)

@@ -7,7 +7,7 @@ fixed batches from tests/golden/ml_like.py instead of the DataLoader's random
 worker sampling, so that igr can be driven with the identical batches,
 identical CPU-generator dropout draws and identical initialisation.
 
-DGL is absent (SURVEY.md §8c); `dgl.ops.gspmm(g,'mul','sum')` is restated as
+DGL is absent; `dgl.ops.gspmm(g,'mul','sum')` is restated as
 a CSR SpMM whose backward is the transposed SpMM (DGL's gspmm semantics; the
 edge values never require grad on this path).  Writes
 tests/golden/train_<shape>.npz (IGCN) and, with `lightgcn`, the reference

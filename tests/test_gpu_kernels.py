@@ -1,6 +1,6 @@
 """GPU parity of the HIP kernels against the CPU oracle (through the C ABI).
 
-Tolerance (fp32, SURVEY.md §8c): |y - y64| <= 1e-5 |y64| + 1e-6 max|y64_row|
+Tolerance (fp32): |y - y64| <= 1e-5 |y64| + 1e-6 max|y64_row|
 against a float64 oracle; integer / index outputs bit-exact.
 """
 import ctypes

@@ -9,7 +9,7 @@ import pytest
 from oracle import igr_oracle as O
 
 # fp32 tolerance for restatements whose summation order differs from the reference run:
-# |y - ref| <= RTOL*|ref| + ATOL_ROW*max|ref_row|  
+# |y - ref| <= RTOL*|ref| + ATOL_ROW*max|ref_row|
 RTOL, ATOL_ROW = 1e-5, 1e-6
 
 

@@ -412,6 +412,21 @@ int igr_adam_f32(int64_t n, float *param, const float *grad, float *exp_avg, flo
                  double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
                  const int64_t *step_dev, void *stream);
 
+/* out[0] = mean(a[0..n)), out[1] = mean(b[0..n)) (b nullable: out[1] untouched):
+ * the means of the per-sample loss and squared-norm terms that
+ * igr_bpr_fwd_bwd_f32 writes (F.softplus(...).mean(), l2_norm_sq.mean();
+ * trainer.py:539-540, 548), in one launch and a fixed summation order. */
+int igr_means_f32(int64_t n, const float *a, const float *b, float *out, void *stream);
+
+/* The step's scalar loss, trainer.py:551-552 (424-425 without the aux term):
+ *     reg_loss = l2_reg * l2 + aux_reg * aux_loss;  loss = bpr_loss + reg_loss
+ * from three device scalars (l2 / aux nullable), each operation rounded on its own
+ * as in the tensor expression; loss_sum (nullable) += loss * weight is the epoch's
+ * running sum (trainer.py:557, losses.update(loss.item(), batch size), kept on
+ * the device). */
+int igr_loss_combine_f32(const float *bpr, const float *l2, const float *aux, float c_l2, float c_aux,
+                         float weight, float *loss, float *loss_sum, void *stream);
+
 /* *counter += value on the stream (one device int64: the step counter a
  * captured training step advances at its end). */
 int igr_counter_add(int64_t *counter, int64_t value, void *stream);

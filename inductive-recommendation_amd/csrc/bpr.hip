@@ -170,6 +170,56 @@ __global__ __launch_bounds__(256) void bpr_finish_kernel(int64_t n, int per, con
     V::store(o, f, seg_run_sum<V, false>(V::load(o, f), n, k, row, keys, terms, ld_terms, f, 1.f));
 }
 
+// out[0] = mean(a), out[1] = mean(b) (b nullable) of n per-sample values, one
+// workgroup, every sum in a fixed order: thread t adds elements t, t + 1024, ...
+// in order, then a fixed tree over the 1024 partials.
+__global__ __launch_bounds__(1024) void means_kernel(int64_t n, const float *__restrict__ a,
+                                                     const float *__restrict__ b, float *__restrict__ out) {
+    __shared__ float red[2][1024];
+    const int t = threadIdx.x;
+    float sa = 0.f, sb = 0.f;
+    for (int64_t i = t; i < n; i += 1024) {
+        sa += a[i];
+        if (b) sb += b[i];
+    }
+    red[0][t] = sa;
+    red[1][t] = sb;
+    __syncthreads();
+    for (int s = 512; s > 0; s >>= 1) {
+        if (t < s) {
+            red[0][t] += red[0][t + s];
+            red[1][t] += red[1][t + s];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        out[0] = red[0][0] / (float)n;
+        if (b) out[1] = red[1][0] / (float)n;
+    }
+}
+
+// reg = c_l2 * l2 + c_aux * aux; loss = bpr + reg (trainer.py:551-552, 424-425),
+// every operation rounded on its own as in the scalar tensor expression, and
+// *loss_sum += loss * weight for the epoch's running sum.
+__global__ void loss_combine_kernel(const float *__restrict__ bpr, const float *__restrict__ l2,
+                                    const float *__restrict__ aux, float c_l2, float c_aux, float weight,
+                                    float *__restrict__ loss, float *__restrict__ loss_sum) {
+    // no contraction into fma: each product and sum is rounded as the tensor ops round them
+#pragma clang fp contract(off)
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    float reg = l2 ? c_l2 * *l2 : 0.f;
+    if (aux) {
+        const float a = c_aux * *aux;
+        reg = l2 ? reg + a : a;
+    }
+    const float v = (l2 || aux) ? *bpr + reg : *bpr;
+    *loss = v;
+    if (loss_sum) {
+        const float add = v * weight;
+        *loss_sum = *loss_sum + add;
+    }
+}
+
 static unsigned grid_for(int64_t n, int block) {
     int64_t g = (n + block - 1) / block;
     if (g > 8192) g = 8192;
@@ -237,5 +287,23 @@ extern "C" int igr_bpr_fwd_bwd_f32(int64_t batch, int32_t d, const int64_t *user
                                    (int64_t)d, grad, ld_grad, grad_blocks, (int)d, dw_part, blocks, dw);
         }
         return launch_status(fn);
+    });
+}
+
+extern "C" int igr_means_f32(int64_t n, const float *a, const float *b, float *out, void *stream) {
+    return guarded("igr_means_f32", [&]() -> int {
+        if (n <= 0 || !a || !out) return arg_error("igr_means_f32", "n <= 0 or a null pointer");
+        hipLaunchKernelGGL(means_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream), n, a, b, out);
+        return launch_status("igr_means_f32");
+    });
+}
+
+extern "C" int igr_loss_combine_f32(const float *bpr, const float *l2, const float *aux, float c_l2, float c_aux,
+                                    float weight, float *loss, float *loss_sum, void *stream) {
+    return guarded("igr_loss_combine_f32", [&]() -> int {
+        if (!bpr || !loss) return arg_error("igr_loss_combine_f32", "bpr and loss must be given");
+        hipLaunchKernelGGL(loss_combine_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), bpr, l2,
+                           aux, c_l2, c_aux, weight, loss, loss_sum);
+        return launch_status("igr_loss_combine_f32");
     });
 }

@@ -96,6 +96,8 @@ SIGNATURES = {
     'igr_adam_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,
                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i64, c_vp, c_vp]),
     'igr_counter_add': (ctypes.c_int, [c_vp, c_i64, c_vp]),
+    'igr_means_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
+    'igr_loss_combine_f32': (ctypes.c_int, [c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

@@ -903,7 +903,8 @@ class BPRLoss(torch.autograd.Function):
         ctx.save_for_backward(t, w, users, pos, neg)
         ctx.off = (int(off_u), int(off_i))
         ctx.distinct = bool(distinct)
-        return loss.mean(), l2.mean()
+        m = means(loss, l2)  # both means in one launch, fixed summation order
+        return m[0], m[1]
 
     @staticmethod
     def backward(ctx, g_loss, g_l2):
@@ -920,6 +921,27 @@ class BPRLoss(torch.autograd.Function):
         _bpr_call(B, t.shape[1], users, pos, neg, ctx.off[0], ctx.off[1], t, w, None, None,
                   0.0 if gl is None else 1.0 / B, 0.0 if g2 is None else 1.0 / B, gl, g2, grad, t.stride(0), dw, keys)
         return grad, dw, None, None, None, None, None, None
+
+
+def means(a, b=None):
+    """[mean(a), mean(b)] of per-sample terms in one launch (igr_means_f32)."""
+    _dev(a, b)
+    a = _f32(a).contiguous()
+    b = None if b is None else _f32(b).contiguous()
+    out = torch.empty(2 if b is not None else 1, dtype=torch.float32, device=a.device)
+    L.call('igr_means_f32', a.numel(), _p(a), _p(b), _p(out), _stream())
+    return out
+
+
+def loss_combine(bpr, l2=None, aux=None, c_l2=0.0, c_aux=0.0, loss_sum=None, weight=1.0):
+    """loss = bpr + (c_l2 * l2 + c_aux * aux) as one launch on detached device
+    scalars (trainer.py:551-552); loss_sum += loss * weight when given."""
+    _dev(bpr, l2, aux, loss_sum)
+    out = torch.empty((), dtype=torch.float32, device=bpr.device)
+    L.call('igr_loss_combine_f32', _p(bpr.detach()), _p(None if l2 is None else l2.detach()),
+           _p(None if aux is None else aux.detach()), float(c_l2), float(c_aux), float(weight), _p(out),
+           _p(loss_sum), _stream())
+    return out
 
 
 def bpr_loss(t, users, pos, neg, off_u, off_i, w=None, distinct=False):

@@ -290,10 +290,9 @@ class StepGraph:
         u, p, ng = tr.sampler.sample(n, offset=self.s0, offset_dev=self.ctr)
         if self.aux is not None:
             au, ap, an = self.aux.sample(n, offset=self.a0, offset_dev=self.ctr)
-            loss = tr.step(u, p, ng, au, ap, an)
+            _summed_step(tr, self.loss_sum, n, u, p, ng, au, ap, an)
         else:
-            loss = tr.step(u, p, ng)
-        self.loss_sum.add_(loss.detach() * n)
+            _summed_step(tr, self.loss_sum, n, u, p, ng)
         L.call('igr_counter_add', ctypes.c_void_p(self.ctr.data_ptr()), 1, ops._stream())
         if count:
             self.n += 1
@@ -341,6 +340,45 @@ def graph_epoch(trainer):
     return sg.take_loss() / total
 
 
+def fused_loss_step(trainer, bpr, l2, aux=None):
+    """loss = bpr + (l2_reg * l2 + aux_reg * aux), its backward and the optimizer
+    step (trainer.py:551-555, 424-428) without scalar tensor arithmetic: the value
+    comes from one kernel and the terms' gradients are the constant coefficients
+    (cached device scalars handed to autograd).  Returns the detached loss."""
+    c_l2 = float(trainer.l2_reg)
+    c_aux = float(getattr(trainer, 'aux_reg', 0.0))
+    acc = getattr(trainer, '_loss_acc', None)
+    loss = ops.loss_combine(bpr, l2, aux, c_l2, c_aux, loss_sum=None if acc is None else acc[0],
+                            weight=1.0 if acc is None else float(acc[1]))
+    trainer._loss_acc = None  # consumed
+    cache = trainer.__dict__.setdefault('_coef_cache', {})
+    terms, grads = [], []
+    for t, c in ((bpr, 1.0), (l2, c_l2), (aux, c_aux)):
+        if t is None or not t.requires_grad:
+            continue
+        if c not in cache:
+            cache[c] = torch.tensor(c, dtype=torch.float32, device=t.device)
+        terms.append(t)
+        grads.append(cache[c])
+    trainer.opt.zero_grad()
+    torch.autograd.backward(terms, grads)
+    trainer.opt.step()
+    return loss
+
+
+def _summed_step(trainer, total, n, *batch):
+    """trainer.step(*batch) with total += loss * n on the device (inside the fused
+    step's combine kernel when there is one); returns the loss."""
+    trainer._loss_acc = (total, n)
+    try:
+        loss = trainer.step(*batch)
+        if trainer._loss_acc is not None:  # not consumed: an unfused step
+            total.add_(loss.detach() * n)
+    finally:
+        trainer._loss_acc = None
+    return loss
+
+
 def base_seed(trainer_config):
     """The trainer's sampling seed: config['seed'], or one drawn from torch's seed
     when the config has none (the reference's configs set none), so that the
@@ -373,7 +411,7 @@ class BPRTrainer(BasicTrainer):
         """One training step on a device batch; returns the loss tensor."""
         if self.fused and hasattr(self.model, 'bpr_loss'):
             bpr_loss, l2 = self.model.bpr_loss(users, pos_items, neg_items)
-            loss = bpr_loss + self.l2_reg * l2
+            return fused_loss_step(self, bpr_loss, l2)
         else:
             users_r, pos_r, neg_r, l2_norm_sq = self.model.bpr_forward(users, pos_items, neg_items)
             pos_scores = torch.sum(users_r * pos_r, dim=1)
@@ -388,11 +426,10 @@ class BPRTrainer(BasicTrainer):
         loss = self._graph_epoch()
         if loss is not None:
             return loss
-        tot, cnt = None, 0
+        tot, cnt = torch.zeros((), dtype=torch.float32, device=self.device), 0
         for batch in self.sampler:
             u, p, n = _dev_batch(batch, self.device)
-            loss = self.step(u, p, n).detach() * len(u)
-            tot = loss if tot is None else tot + loss
+            _summed_step(self, tot, len(u), u, p, n)
             cnt += len(u)
         return float(tot) / cnt
 
@@ -419,6 +456,7 @@ class IGCNTrainer(BasicTrainer):
         m = self.model
         if self.fused:
             bpr_loss, l2, aux_loss = m.bpr_aux_loss(users, pos_items, neg_items, a_users, a_pos, a_neg)
+            return fused_loss_step(self, bpr_loss, l2, aux_loss)
         else:
             users_r, pos_r, neg_r, l2_norm_sq = m.bpr_forward(users, pos_items, neg_items)
             bpr_loss = F.softplus(torch.sum(users_r * neg_r, 1) - torch.sum(users_r * pos_r, 1)).mean()
@@ -427,7 +465,7 @@ class IGCNTrainer(BasicTrainer):
             pe = m.embedding(a_pos + len(m.user_map))
             ne = m.embedding(a_neg + len(m.user_map))
             aux_loss = F.softplus(torch.sum(ue * ne * m.w[None, :], 1) - torch.sum(ue * pe * m.w[None, :], 1)).mean()
-        loss = bpr_loss + self.l2_reg * l2 + self.aux_reg * aux_loss
+        loss = bpr_loss + (self.l2_reg * l2 + self.aux_reg * aux_loss)
         self.opt.zero_grad()
         loss.backward()
         self.opt.step()
@@ -438,12 +476,11 @@ class IGCNTrainer(BasicTrainer):
         if loss is not None:
             self.model.feat_mat_anneal()
             return loss
-        tot, cnt = None, 0
+        tot, cnt = torch.zeros((), dtype=torch.float32, device=self.device), 0
         for main, aux in zip(self.sampler, self.aux_sampler):
             u, p, n = _dev_batch(main, self.device)
             au, ap, an = _dev_batch(aux, self.device)
-            loss = self.step(u, p, n, au, ap, an).detach() * len(au)
-            tot = loss if tot is None else tot + loss
+            _summed_step(self, tot, len(au), u, p, n, au, ap, an)
             cnt += len(au)
         self.model.feat_mat_anneal()
         return float(tot) / cnt

@@ -215,6 +215,8 @@ def test_new_entry_points_validate_arguments():
     _refused('igr_dropout_uniforms', None, 1, 0, None, 0, F, st, match='NULL')
     # hipGraph-step entry points: the device counter, Adam's host step without one, per-head SpMM
     _refused('igr_counter_add', None, 1, st, match='NULL')
+    _refused('igr_means_f32', 0, F, None, F, st, match='n <= 0')
+    _refused('igr_loss_combine_f32', None, None, None, 0.0, 0.0, 1.0, F, None, st, match='bpr')
     _refused('igr_adam_f32', 4, F, F, F, F, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None, st, match='step')
     _refused('igr_bpr_sample', 4, 0, F, F, F, 10, 1, 0, None, 8, F, F, F, st, match='active')
     _refused('igr_spmm_heads_f32', ctypes.byref(rect.csr), 4, 64, F, 64, F, F, 256, None, st, match='leading')

@@ -953,3 +953,32 @@ def test_sddmm_shared_source_and_its_gradient(h, d, dedup):
     ut = t(u).requires_grad_(True)
     (ops.GSDDMMShared.apply(g, ut, t(v), h) * t(rhs)).sum().backward()
     assert torch.equal(ut.grad, y)
+
+
+@pytest.mark.parametrize('n', [1, 7, 1024, 2048, 5001])
+def test_means_of_loss_terms(n):
+    """mean(a), mean(b) in one launch: against float64, equal on repeated calls, b optional."""
+    rng = np.random.default_rng(n)
+    a = rng.standard_normal(n).astype(np.float32) + 0.7
+    b = (rng.standard_normal(n).astype(np.float32)) ** 2
+    m = ops.means(t(a), t(b))
+    np.testing.assert_allclose(m.cpu().numpy(), [a.astype(np.float64).mean(), b.astype(np.float64).mean()], rtol=2e-6)
+    assert torch.equal(m, ops.means(t(a), t(b)))
+    m1 = ops.means(t(a))
+    assert m1.shape == (1,) and torch.equal(m1[0], m[0])
+
+
+def test_loss_combine_is_the_reference_expression_bitwise():
+    """loss = bpr + (l2_reg * l2 + aux_reg * aux) (trainer.py:551-552) with every operation
+    rounded on its own, and the running sum += loss * n, against the same tensor expression."""
+    rng = np.random.default_rng(5)
+    for _ in range(20):
+        bpr, l2, aux = (torch.tensor(float(v), device=DEV) for v in rng.standard_normal(3).astype(np.float32))
+        c_l2, c_aux, n = float(np.float32(rng.random())), float(np.float32(rng.random() * 0.1)), int(rng.integers(1, 4096))
+        tot = torch.tensor(float(np.float32(rng.standard_normal())), device=DEV)
+        ref = bpr + (c_l2 * l2 + c_aux * aux)
+        ref_tot = tot + ref * n
+        got = ops.loss_combine(bpr, l2, aux, c_l2, c_aux, loss_sum=tot, weight=n)
+        assert torch.equal(got, ref) and torch.equal(tot, ref_tot)
+        assert torch.equal(ops.loss_combine(bpr, l2, None, c_l2), bpr + c_l2 * l2)   # BPRTrainer, trainer.py:424-425
+        assert torch.equal(ops.loss_combine(bpr), bpr)

@@ -15,96 +15,151 @@
 //   igr_spmm_shared_heads_f32   y[r, h, :]  = sum_{e in row r} rhs[eid, h] * x[c, :]
 //                               (its gradient with respect to u)
 // Both: one wave per destination row, d / 4 lanes per source row (one 16-byte load
-// per lane), 64 / (d / 4) edges side by side, UE edges per lane group in flight.
+// per lane), 64 / (d / 4) edges side by side, several edges per lane group in flight.
 #include "common.h"
 
 namespace igr {
 
-// Edges per lane group per trip.  Measured on MI355X (nnz 411 M, h = 4, d = 64):
-// 1 -> 24.6 ms, 2 -> 26.9, 4 -> 46.8, 8 -> 134: the kernel is bound by the work its
-// lanes do on a trip's empty slots (rows of ~20 edges fill few of a wide trip) and by
-// registers, not by gathers in flight.
+// Edges per lane group per trip (0: chosen per width so that a trip covers 16 edges,
+// at most 4 per group) and trips whose gathers are all issued before the first of them
+// is reduced (a scheduling barrier keeps them there).  A trip's loads are
+// unconditional - an empty slot re-reads the row's last edge, an L2 hit - because a
+// load under a lane condition whose other arm zeroes the register is followed by a
+// wait at the join: with such loads the kernel ran with one 16-byte gather in flight
+// per lane (24.5 ms at nnz 411 M, h = 4, d = 64, and slower the more edges a trip took).
+// Measured on MI355X with the loads unconditional (U x NT): 1x4 19.8 ms, 4x1 19.8, 2x2 19.9,
+// 2x3 20.0, 1x6 20.2, 4x2 20.3, 1x8 20.4, 1x2 21.2, 4x4 23.5 (133 VGPRs: 3 waves per SIMD).
 #ifndef IGR_SDDMM_SHARED_U
 #define IGR_SDDMM_SHARED_U 1
 #endif
+#ifndef IGR_SDDMM_SHARED_NT
+#define IGR_SDDMM_SHARED_NT 4
+#endif
+static_assert(IGR_SDDMM_SHARED_NT >= 1 && IGR_SDDMM_SHARED_NT <= 8, "1 to 8 trips per pass");
 
-constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v >> 1); }
+typedef float v4f __attribute__((ext_vector_type(4)));
 
-template <int D, int H>
+// x of the lane that a DPP control selects (quad permutes and row mirrors: every
+// lane has a source, no LDS traffic)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, true));
+}
+
+// Sum of x over the LPE (a power of two) consecutive lanes of a group, left in every one
+// of them: xor 1 and xor 2 inside quads, then the mirrored half of 8 and of 16 lanes
+// (the partial sums are uniform inside what is mirrored), shuffles beyond a row.
+template <int LPE>
+__device__ __forceinline__ float group_sum(float x) {
+    if (LPE >= 2) x += dpp_f<0xB1>(x);   // quad_perm [1, 0, 3, 2]
+    if (LPE >= 4) x += dpp_f<0x4E>(x);   // quad_perm [2, 3, 0, 1]
+    if (LPE >= 8) x += dpp_f<0x141>(x);  // row_half_mirror
+    if (LPE >= 16) x += dpp_f<0x140>(x); // row_mirror
+    if (LPE >= 32) x += shfl_xor_f(x, 16);
+    if (LPE >= 64) x += shfl_xor_f(x, 32);
+    return x;
+}
+
+template <int D, int H, bool EID>
+struct SddmmShared {
+    static constexpr int LPE = D / 4;    // lanes per edge (source row)
+    static constexpr int EPW = 64 / LPE; // edges side by side in a wave
+    static constexpr int UE = IGR_SDDMM_SHARED_U > 0 ? IGR_SDDMM_SHARED_U : (16 / EPW < 1 ? 1 : (16 / EPW > 4 ? 4 : 16 / EPW));
+    static constexpr int TRIP = UE * EPW;  // edges per trip (divides 64)
+    static constexpr int NT = IGR_SDDMM_SHARED_NT < 64 / TRIP ? IGR_SDDMM_SHARED_NT : 64 / TRIP;  // trips per pass
+
+    // NTR trips starting at edge t0 of the block: every gather first, then each trip's
+    // dots, their sums over the group's lanes and the stores (lane 0 of the group
+    // writes the H scores of each of its UE edges)
+    template <int NTR>
+    static __device__ __forceinline__ void pass(int t0, int n, int cl, int eg, int sub, const v4f (&uq)[H],
+                                                const float *__restrict__ vs, int ld_v,
+                                                const int64_t *__restrict__ eid, int64_t base,
+                                                float *__restrict__ out) {
+        v4f vk[NTR][UE];
+#pragma unroll
+        for (int tt = 0; tt < NTR; ++tt)
+#pragma unroll
+            for (int j = 0; j < UE; ++j) {
+                const int k = t0 + tt * TRIP + eg * UE + j;
+                const int c = shfl_i(cl, k < n ? k : n - 1);
+                vk[tt][j] = *reinterpret_cast<const v4f *>(vs + (int64_t)c * ld_v);
+            }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int tt = 0; tt < NTR; ++tt) {
+            const int k0 = t0 + tt * TRIP + eg * UE;
+            float sv[UE][H];
+#pragma unroll
+            for (int j = 0; j < UE; ++j)
+#pragma unroll
+                for (int hh = 0; hh < H; ++hh)
+                    sv[j][hh] = group_sum<LPE>(uq[hh].x * vk[tt][j].x + uq[hh].y * vk[tt][j].y +
+                                               uq[hh].z * vk[tt][j].z + uq[hh].w * vk[tt][j].w);
+            if (sub == 0) {
+#pragma unroll
+                for (int j = 0; j < UE; ++j) {
+                    const int k = k0 + j;
+                    if (k >= n) continue;
+                    float *o = out + (EID ? eid[base + k] : base + k) * H;
+                    if (H % 4 == 0) {
+#pragma unroll
+                        for (int q = 0; q < H / 4; ++q)
+                            reinterpret_cast<v4f *>(o)[q] = v4f{sv[j][4 * q], sv[j][4 * q + 1], sv[j][4 * q + 2], sv[j][4 * q + 3]};
+                    } else {
+#pragma unroll
+                        for (int hh = 0; hh < H; ++hh) o[hh] = sv[j][hh];
+                    }
+                }
+            }
+        }
+    }
+};
+
+template <int D, int H, bool EID>
 __global__ __launch_bounds__(256) void sddmm_shared_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr,
                                                            const int32_t *__restrict__ col,
                                                            const int64_t *__restrict__ eid,
                                                            const float *__restrict__ u, int64_t ld_u,
-                                                           const float *__restrict__ v, int64_t ld_v,
+                                                           const float *__restrict__ v, int ld_v,
                                                            float *__restrict__ out) {
-    constexpr int LPE = D / 4;               // lanes per edge (source row)
-    constexpr int EPW = 64 / LPE;            // edges side by side in a wave
-    constexpr int UE = IGR_SDDMM_SHARED_U;   // edges per lane group per trip
-    constexpr int TRIP = UE * EPW;           // edges per trip (divides 64)
-    constexpr int V = UE * H;                // partial dots a lane holds: [edge][head]
-    constexpr int RS = ilog2(V) < ilog2(LPE) ? ilog2(V) : ilog2(LPE);  // reduce-scatter steps
-    constexpr int R = V >> RS;               // finished values per writer lane
+    using S = SddmmShared<D, H, EID>;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n_rows) return;
     const int lane = threadIdx.x & 63;
-    const int eg = lane / LPE;
-    const int sub = lane - eg * LPE;
-    float4 uq[H];
+    const int eg = lane / S::LPE;
+    const int sub = lane - eg * S::LPE;
+    v4f uq[H];
 #pragma unroll
-    for (int hh = 0; hh < H; ++hh) uq[hh] = *reinterpret_cast<const float4 *>(u + r * ld_u + hh * D + sub * 4);
+    for (int hh = 0; hh < H; ++hh) uq[hh] = *reinterpret_cast<const v4f *>(u + r * ld_u + hh * D + sub * 4);
     const float *vs = v + sub * 4;
     const int64_t b = row_ptr[r], e = row_ptr[r + 1];
     for (int64_t base = b; base < e; base += 64) {
         const int n = (int)min((int64_t)64, e - base);
         const int cl = lane < n ? col[base + lane] : 0;
-        for (int t = 0; t < n; t += TRIP) {
-            const int k0 = t + eg * UE;  // this group's first edge in the block
-            float4 vk[UE];
-#pragma unroll
-            for (int j = 0; j < UE; ++j) {
-                const int c = shfl_i(cl, (k0 + j) & 63);
-                vk[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (k0 + j < n) vk[j] = *reinterpret_cast<const float4 *>(vs + (int64_t)c * ld_v);
-            }
-            float sv[V];
-#pragma unroll
-            for (int j = 0; j < UE; ++j)
-#pragma unroll
-                for (int hh = 0; hh < H; ++hh)
-                    sv[j * H + hh] = uq[hh].x * vk[j].x + uq[hh].y * vk[j].y + uq[hh].z * vk[j].z + uq[hh].w * vk[j].w;
-            // butterfly reduce-scatter over the group's LPE lanes: at each step a lane keeps
-            // one half of its values and adds the partner's copy of that half, so after RS
-            // steps it holds R values summed over 2^RS lanes; value index = (top RS bits of
-            // sub) * R + i
-#pragma unroll
-            for (int s = 0, cnt = V; s < RS; ++s, cnt >>= 1) {
-                const int m = LPE >> (s + 1);
-                const bool hi = (sub & m) != 0;
-#pragma unroll
-                for (int i = 0; i < cnt / 2; ++i) {
-                    const float keep = hi ? sv[i + cnt / 2] : sv[i];
-                    const float send = hi ? sv[i] : sv[i + cnt / 2];
-                    sv[i] = keep + shfl_xor_f(send, m);
-                }
-            }
-            // lanes left over (fewer values than lanes): plain xor steps
-#pragma unroll
-            for (int m = (LPE >> RS) >> 1; m >= 1; m >>= 1)
-#pragma unroll
-                for (int i = 0; i < R; ++i) sv[i] += shfl_xor_f(sv[i], m);
-            if ((sub & ((LPE >> RS) - 1)) == 0) {
-                const int first = (sub >> (ilog2(LPE) - RS)) * R;
-#pragma unroll
-                for (int i = 0; i < R; ++i) {
-                    const int idx = first + i, j = idx / H, hh = idx - j * H;
-                    const int k = k0 + j;
-                    if (k < n) out[(eid ? eid[base + k] : base + k) * H + hh] = sv[i];
-                }
-            }
+        // n is the same in every lane: the number of trips left picks a straight-line pass
+        for (int t0 = 0; t0 < n; t0 += S::NT * S::TRIP) {
+            const int left = (n - t0 + S::TRIP - 1) / S::TRIP;
+            const int nt = left < S::NT ? left : S::NT;
+#define IGR_PASS(N_) S::template pass<(S::NT >= N_ ? N_ : 1)>(t0, n, cl, eg, sub, uq, vs, ld_v, eid, base, out)
+            if (nt == 8) IGR_PASS(8);
+            else if (nt == 7) IGR_PASS(7);
+            else if (nt == 6) IGR_PASS(6);
+            else if (nt == 5) IGR_PASS(5);
+            else if (nt == 4) IGR_PASS(4);
+            else if (nt == 3) IGR_PASS(3);
+            else if (nt == 2) IGR_PASS(2);
+            else IGR_PASS(1);
+#undef IGR_PASS
         }
     }
 }
 
+// Edges per lane group per trip of the gradient kernel, measured on MI355X (nnz 411 M,
+// h = 4, d = 64): 1 -> 19.4 ms, 2 -> 18.6, 4 -> 19.6, 8 -> 22.8.
+#ifndef IGR_SPMM_SHARED_U
+#define IGR_SPMM_SHARED_U 2
+#endif
 // y[r, hh, :] = sum over the edges of row r of rhs[eid, hh] * x[col, :]: each source row
 // is gathered once and feeds H accumulators; the EPW lane groups take alternate edges
 // and are summed in a fixed xor tree at the end (deterministic).
@@ -112,12 +167,12 @@ template <int D, int H>
 __global__ __launch_bounds__(256) void spmm_shared_heads_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr,
                                                                 const int32_t *__restrict__ col,
                                                                 const int64_t *__restrict__ eid,
-                                                                const float *__restrict__ x, int64_t ldx,
+                                                                const float *__restrict__ x, int ldx,
                                                                 const float *__restrict__ rhs,
                                                                 float *__restrict__ y, int64_t ldy) {
     constexpr int LPE = D / 4;
     constexpr int EPW = 64 / LPE;
-    constexpr int UE = 4;
+    constexpr int UE = IGR_SPMM_SHARED_U;
     constexpr int TRIP = UE * EPW;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n_rows) return;
@@ -135,26 +190,38 @@ __global__ __launch_bounds__(256) void spmm_shared_heads_kernel(int64_t n_rows, 
         const int64_t el = lane < n ? (eid ? eid[base + lane] : base + lane) : 0;
         for (int t = 0; t < n; t += TRIP) {
             const int k0 = t + eg * UE;
-            float4 xv[UE];
+            v4f xv[UE];
+            v4f wq[UE][(H + 3) / 4];
             float wv[UE][H];
+            // every load of the trip is unconditional (an empty slot re-reads the row's last
+            // edge and its weights are replaced by zeros), so all of them are in flight at once
 #pragma unroll
             for (int j = 0; j < UE; ++j) {
-                const int src = (k0 + j) & 63;
+                const int src = k0 + j < n ? k0 + j : n - 1;
                 const int c = shfl_i(cl, src);
                 const int64_t ee = ((int64_t)shfl_i((int)(el >> 32), src) << 32) | (uint32_t)shfl_i((int)el, src);
-                xv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                xv[j] = *reinterpret_cast<const v4f *>(xs + (int64_t)c * ldx);
+                if (H % 4 == 0) {
 #pragma unroll
-                for (int hh = 0; hh < H; ++hh) wv[j][hh] = 0.f;
-                if (k0 + j < n) {
-                    xv[j] = *reinterpret_cast<const float4 *>(xs + (int64_t)c * ldx);
+                    for (int q = 0; q < H / 4; ++q) wq[j][q] = reinterpret_cast<const v4f *>(rhs + ee * H)[q];
+                } else {
 #pragma unroll
                     for (int hh = 0; hh < H; ++hh) wv[j][hh] = rhs[ee * H + hh];
                 }
             }
 #pragma unroll
-            for (int j = 0; j < UE; ++j)
+            for (int j = 0; j < UE; ++j) {
+                const bool valid = k0 + j < n;
 #pragma unroll
-                for (int hh = 0; hh < H; ++hh) acc[hh] = f4_fma(wv[j][hh], xv[j], acc[hh]);
+                for (int hh = 0; hh < H; ++hh) {
+                    const float w = H % 4 == 0 ? wq[j][hh / 4][hh % 4] : wv[j][hh];
+                    const float wz = valid ? w : 0.f;
+                    acc[hh].x = fmaf(wz, xv[j].x, acc[hh].x);
+                    acc[hh].y = fmaf(wz, xv[j].y, acc[hh].y);
+                    acc[hh].z = fmaf(wz, xv[j].z, acc[hh].z);
+                    acc[hh].w = fmaf(wz, xv[j].w, acc[hh].w);
+                }
+            }
         }
     }
 #pragma unroll
@@ -187,8 +254,13 @@ template <int D, int H>
 struct LaunchSddmmShared {
     static void go(const igr_csr *g, const float *u, int64_t ld_u, const float *v, int64_t ld_v, float *out,
                    hipStream_t st) {
-        hipLaunchKernelGGL((sddmm_shared_kernel<D, H>), dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0, st,
-                           g->n_rows, g->row_ptr, g->col_idx, g->edge_id, u, ld_u, v, ld_v, out);
+        const dim3 grid((unsigned)((g->n_rows + 3) / 4));
+        if (g->edge_id)
+            hipLaunchKernelGGL((sddmm_shared_kernel<D, H, true>), grid, dim3(256), 0, st, g->n_rows, g->row_ptr,
+                               g->col_idx, g->edge_id, u, ld_u, v, (int)ld_v, out);
+        else
+            hipLaunchKernelGGL((sddmm_shared_kernel<D, H, false>), grid, dim3(256), 0, st, g->n_rows, g->row_ptr,
+                               g->col_idx, g->edge_id, u, ld_u, v, (int)ld_v, out);
     }
 };
 
@@ -197,7 +269,7 @@ struct LaunchSpmmShared {
     static void go(const igr_csr *g, const float *x, int64_t ldx, const float *rhs, float *y, int64_t ldy,
                    hipStream_t st) {
         hipLaunchKernelGGL((spmm_shared_heads_kernel<D, H>), dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0, st,
-                           g->n_rows, g->row_ptr, g->col_idx, g->edge_id, x, ldx, rhs, y, ldy);
+                           g->n_rows, g->row_ptr, g->col_idx, g->edge_id, x, (int)ldx, rhs, y, ldy);
     }
 };
 
@@ -215,6 +287,8 @@ extern "C" int igr_sddmm_shared_f32(const igr_csr *g, int32_t h, int32_t d, cons
         if (!u || !v || !out) return arg_error(fn, "NULL pointer");
         if (ld_u % 4 || ld_v % 4 || !aligned16(u) || !aligned16(v))
             return arg_error(fn, "u / v must be 16-byte aligned with leading dimensions a multiple of 4");
+        if (ld_v > 2147483647) return arg_error(fn, "ld_v too large");
+        if (h % 4 == 0 && !aligned16(out)) return arg_error(fn, "out must be 16-byte aligned");
         if (!dispatch_dh<LaunchSddmmShared>(d, h, g, u, ld_u, v, ld_v, out, reinterpret_cast<hipStream_t>(stream)))
             return arg_error(fn, "supported: d in {32, 64, 128, 256} with h * d <= 512, h a power of two");
         return launch_status(fn);
@@ -231,6 +305,8 @@ extern "C" int igr_spmm_shared_heads_f32(const igr_csr *g, int32_t h, int32_t d,
         if (!y || (g->nnz > 0 && (!x || !rhs))) return arg_error(fn, "NULL pointer");
         if (ldx % 4 || ldy % 4 || !aligned16(x) || !aligned16(y))
             return arg_error(fn, "x / y must be 16-byte aligned with leading dimensions a multiple of 4");
+        if (ldx > 2147483647) return arg_error(fn, "ldx too large");
+        if (h % 4 == 0 && g->nnz > 0 && !aligned16(rhs)) return arg_error(fn, "rhs must be 16-byte aligned");
         if (!dispatch_dh<LaunchSpmmShared>(d, h, g, x, ldx, rhs, y, ldy, reinterpret_cast<hipStream_t>(stream)))
             return arg_error(fn, "supported: d in {32, 64, 128, 256} with h * d <= 512, h a power of two");
         return launch_status(fn);

@@ -154,9 +154,11 @@ class LightGCN(BasicModel):
         users_r = ops.gather(rep, users)
         return ops.gemm(users_r, rep[self.n_users:])
 
-    def bpr_loss(self, users, pos_items, neg_items):
+    def bpr_loss(self, users, pos_items, neg_items, need_l2=True):
         """Fused LightGCN/BPRTrainer step terms: (bpr loss, mean l2 of raw embeddings).
-        The last layer runs only at the batch rows when batch_rep_pays."""
+        The last layer runs only at the batch rows when batch_rep_pays.  need_l2=False
+        (a trainer whose l2_reg is 0: the term and its gradient are exact zeros) skips
+        the l2 pass and returns None for it."""
         if batch_rep_pays(self, users.numel()):
             rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
             rep_b = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
@@ -165,6 +167,8 @@ class LightGCN(BasicModel):
         else:
             rep = self.get_rep()
             bpr, _ = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
+        if not need_l2:
+            return bpr, None
         _, l2 = ops.bpr_loss(self.embedding.weight, users, pos_items, neg_items, 0, self.n_users)
         return bpr, l2
 
@@ -388,9 +392,11 @@ class IGCN(BasicModel):
     def _l2_extra(self):
         return None
 
-    def bpr_loss(self, users, pos_items, neg_items):
+    def bpr_loss(self, users, pos_items, neg_items, need_l2=True):
         """Fused IGCNTrainer terms on rep: (bpr loss, mean l2 of rep rows).
-        The last layer runs only at the batch rows when batch_rep_pays."""
+        The last layer runs only at the batch rows when batch_rep_pays.  need_l2=False
+        (l2_reg = 0, as in the reference's IGCN configs: the term and its gradient are
+        exact zeros) returns None for l2 and skips AttIGCN's projection norms."""
         if self._rows_path(users.numel()):
             rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
             rep_b = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
@@ -398,21 +404,25 @@ class IGCN(BasicModel):
             bpr, l2 = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0, distinct=True)
         else:
             bpr, l2 = ops.bpr_loss(self.get_rep(), users, pos_items, neg_items, 0, self.n_users)
+        if not need_l2:
+            return bpr, None
         extra = self._l2_extra()
         return bpr, (l2 if extra is None else l2 + extra)
 
-    def bpr_aux_loss(self, users, pos_items, neg_items, a_users, a_pos, a_neg):
+    def bpr_aux_loss(self, users, pos_items, neg_items, a_users, a_pos, a_neg, need_l2=True):
         """All three IGCNTrainer.step terms (trainer.py:536-549): (bpr, l2, aux).
         On the row path the aux term rides in the same autograd node, so its
         gradient is added into the embedding gradient in place."""
         if not self._rows_path(users.numel()):
-            bpr, l2 = self.bpr_loss(users, pos_items, neg_items)
+            bpr, l2 = self.bpr_loss(users, pos_items, neg_items, need_l2)
             return bpr, l2, self.aux_loss(a_users, a_pos, a_neg)
         rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
         rep_b, aux = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
                                         feat=self.feat_mat, fvals=self.inductive_values(), adj_vals=self.norm_vals,
                                         aux=(a_users, a_pos, a_neg, len(self.user_map)), w=self.w)
         bpr, l2 = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0, distinct=True)
+        if not need_l2:
+            return bpr, None, aux
         extra = self._l2_extra()
         return bpr, (l2 if extra is None else l2 + extra), aux
 

@@ -354,7 +354,7 @@ def fused_loss_step(trainer, bpr, l2, aux=None):
     cache = trainer.__dict__.setdefault('_coef_cache', {})
     terms, grads = [], []
     for t, c in ((bpr, 1.0), (l2, c_l2), (aux, c_aux)):
-        if t is None or not t.requires_grad:
+        if t is None or not t.requires_grad or c == 0.0:  # a zero coefficient: exact-zero gradients
             continue
         if c not in cache:
             cache[c] = torch.tensor(c, dtype=torch.float32, device=t.device)
@@ -410,7 +410,7 @@ class BPRTrainer(BasicTrainer):
     def step(self, users, pos_items, neg_items):
         """One training step on a device batch; returns the loss tensor."""
         if self.fused and hasattr(self.model, 'bpr_loss'):
-            bpr_loss, l2 = self.model.bpr_loss(users, pos_items, neg_items)
+            bpr_loss, l2 = self.model.bpr_loss(users, pos_items, neg_items, need_l2=self.l2_reg != 0)
             return fused_loss_step(self, bpr_loss, l2)
         else:
             users_r, pos_r, neg_r, l2_norm_sq = self.model.bpr_forward(users, pos_items, neg_items)
@@ -455,7 +455,8 @@ class IGCNTrainer(BasicTrainer):
     def step(self, users, pos_items, neg_items, a_users, a_pos, a_neg):
         m = self.model
         if self.fused:
-            bpr_loss, l2, aux_loss = m.bpr_aux_loss(users, pos_items, neg_items, a_users, a_pos, a_neg)
+            bpr_loss, l2, aux_loss = m.bpr_aux_loss(users, pos_items, neg_items, a_users, a_pos, a_neg,
+                                                    need_l2=self.l2_reg != 0)
             return fused_loss_step(self, bpr_loss, l2, aux_loss)
         else:
             users_r, pos_r, neg_r, l2_norm_sq = m.bpr_forward(users, pos_items, neg_items)

@@ -23,6 +23,10 @@ import os
 import sys
 import time
 
+# the host driver supports only dmabuf IPC: without this RCCL's buffer exchange between the
+# ranks' processes fails (hipIpcGetMemHandle: invalid argument); must be set before HIP starts
+os.environ.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'inductive-recommendation_amd'))
 sys.path.insert(0, ROOT)

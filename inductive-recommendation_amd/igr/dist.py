@@ -267,6 +267,9 @@ def _col_width(d, table_bytes):
     """Column width per pass of a wide-row SpMM: 128 when d = 256 and the gathered
     table outgrows the Infinity Cache, so each pass gathers from a slice half as
     large (same sums, column by column); d otherwise."""
+    forced = int(os.environ.get('IGR_COL_WIDTH', '0'))  # tuning override (scripts / bench experiments)
+    if forced > 0 and d % forced == 0:
+        return forced
     return 128 if (d == 256 and table_bytes > MALL_BYTES) else d
 
 

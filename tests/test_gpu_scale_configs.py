@@ -3,6 +3,7 @@
     MovieLens-1M shape, d = 64, 2 layers, attention SpMM   AttIGCN  model.py:4223-4287
     Gowalla shape (29,858 x 40,981, ~1.04 M), d = 128, L = 3  IGCN     model.py:4188-4200, config.py:12-23
     synthetic scale, d = 256, the sharded layer with 128-column passes
+    the bench workload itself (10 M x 1 M, 200 M draws, d = 64) through size-independent properties
     items outnumbering users (Amazon-Books-shaped), items sharded at world 2 on one GPU
 
 The first two compare against fixtures written by tests/golden/make_scale_golden.py,
@@ -194,6 +195,70 @@ def test_sharded_layer_d256_column_passes_at_scale():
         vu, vi = sh.layer(xu, xi)
     finally:
         dist._col_width = one
+    assert torch.equal(vu, yu) and torch.equal(vi, yi)
+
+
+def test_bench_workload_full_size_properties():
+    """The bench workload itself (10 M users x 1 M items, 200 M draws, d = 64: the graph, the
+    values and the launches bench.py times), checked through properties that need no
+    second full-size implementation:
+      * a known answer: sqrt(degree) is an eigenvector of D^-1/2 A D^-1/2 with eigenvalue 1
+        (utils.py:42-50), so layer(sqrt(deg)) = sqrt(deg) on every node with an interaction;
+      * float64 on sampled rows of both sides, from the host CSR;
+      * the adjoint identity <x_u, A_ui x_i> = <A_iu x_u, x_i> ties the two blocks together;
+      * column checksums: 1^T (A x) = (A^T 1)^T x with the column sums of A taken on the host;
+      * linearity, and the same bits on a second run."""
+    from igr import dist
+    from igr.dataset import synthetic_pairs
+    U, I, E, d = 10_000_000, 1_000_000, 200_000_000, 64
+    pairs = synthetic_pairs(U, I, E, 0, 'uniform')
+    sh = dist.BipartiteShard(pairs, U, I, 0, 1, DEV, d=d)
+    del pairs
+    assert sh.local_nnz == 399_995_952 and sh.item_tiles == 4  # the graph and the tiling of the bench line
+    deg = torch.from_numpy(sh.degree).to(DEV)
+    # known answer (fp32 values: three roundings per edge, ~20 to ~200 terms per row)
+    su, si = deg[:U].sqrt()[:, None].repeat(1, d).contiguous(), deg[U:].sqrt()[:, None].repeat(1, d).contiguous()
+    eu, ei = sh.layer(su, si)
+    for got, ref in [(eu, su), (ei, si)]:
+        assert float(((got - ref).abs() / ref.clamp_min(1.0)).max()) <= 1e-5
+    del su, si, eu, ei
+    g = torch.Generator(device=DEV).manual_seed(2)
+    xu, xi = torch.randn(U, d, generator=g, device=DEV) * 0.1, torch.randn(I, d, generator=g, device=DEV) * 0.1
+    yu, yi = sh.layer(xu, xi)
+    # sampled rows in float64
+    rng = np.random.default_rng(0)
+    ub, ih = sh.user_block.host(), sh.item_host
+    uv, iv = sh.user_vals.cpu().numpy(), ih['vals']
+    for r in rng.integers(0, U, 200):
+        b, e = int(ub['row_ptr'][r]), int(ub['row_ptr'][r + 1])
+        src = xi[torch.from_numpy(ub['col_idx'][b:e].astype(np.int64)).to(DEV)].cpu().numpy().astype(np.float64)
+        close(yu[r].cpu().numpy()[None], (uv[b:e, None].astype(np.float64) * src).sum(0)[None])
+    for r in rng.integers(0, I, 200):
+        b, e = int(ih['row_ptr'][r]), int(ih['row_ptr'][r + 1])
+        src = xu[torch.from_numpy(ih['col_idx'][b:e].astype(np.int64)).to(DEV)].cpu().numpy().astype(np.float64)
+        close(yi[r].cpu().numpy()[None], (iv[b:e, None].astype(np.float64) * src).sum(0)[None], atol_row=2e-6)
+    # adjoint identity between the user block and the item block (A symmetric)
+    lhs = float((xu.double() * yu.double()).sum())   # <x_u, A_ui x_i>
+    rhs = float((yi.double() * xi.double()).sum())   # <A_iu x_u, x_i>
+    scale = float((xu.double().abs() * yu.double().abs()).sum())
+    assert abs(lhs - rhs) <= 1e-6 * scale
+    # column checksums against host column sums of the values (float64)
+    cs_items = np.bincount(ub['col_idx'], weights=uv.astype(np.float64), minlength=I)   # A_ui^T 1
+    cs_users = np.bincount(ih['col_idx'], weights=iv.astype(np.float64), minlength=U)   # A_iu^T 1
+    for y, cs, x in [(yu, cs_items, xi), (yi, cs_users, xu)]:
+        got = y.double().sum(0).cpu().numpy()
+        w = torch.from_numpy(cs).to(DEV)
+        ref = (w[:, None] * x.double()).sum(0).cpu().numpy()
+        mag = float((w[:, None] * x.double().abs()).sum(0).max())
+        assert np.abs(got - ref).max() <= 1e-6 * mag
+    # linearity and repeatability
+    zu, zi = torch.randn(U, d, generator=g, device=DEV) * 0.1, torch.randn(I, d, generator=g, device=DEV) * 0.1
+    wu, wi = sh.layer(zu, zi)
+    cu, ci = sh.layer(0.5 * xu - 2.0 * zu, 0.5 * xi - 2.0 * zi)
+    for got, a, b in [(cu, yu, wu), (ci, yi, wi)]:
+        ref = 0.5 * a.double() - 2.0 * b.double()
+        assert float((got.double() - ref).abs().max()) <= 2e-6 * float(ref.abs().max())
+    vu, vi = sh.layer(xu, xi)
     assert torch.equal(vu, yu) and torch.equal(vi, yi)
 
 

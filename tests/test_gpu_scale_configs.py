@@ -4,6 +4,7 @@
     Gowalla shape (29,858 x 40,981, ~1.04 M), d = 128, L = 3  IGCN     model.py:4188-4200, config.py:12-23
     synthetic scale, d = 256, the sharded layer with 128-column passes
     the bench workload itself (10 M x 1 M, 200 M draws, d = 64) through size-independent properties
+    the attention edge kernels on that graph's feature graph (nnz 411 M, 4 heads of d = 64), likewise
     items outnumbering users (Amazon-Books-shaped), items sharded at world 2 on one GPU
 
 The first two compare against fixtures written by tests/golden/make_scale_golden.py,
@@ -260,6 +261,73 @@ def test_bench_workload_full_size_properties():
         assert float((got.double() - ref).abs().max()) <= 2e-6 * float(ref.abs().max())
     vu, vi = sh.layer(xu, xi)
     assert torch.equal(vu, yu) and torch.equal(vi, yi)
+
+
+def test_attention_kernels_full_size_properties():
+    """The attention inductive layer's edge kernels on IGCN's feature graph of the synthetic
+    bipartite graph (11 M nodes, nnz 411 M, 4 heads of d = 64; model.py:4246-4275):
+      * shared-source SDDMM on sampled edges against float64;
+      * the adjoint identity sum_{r,h} <u[r,h], y[r,h]> = sum_{e,h} rhs[e,h] out[e,h] between
+        the SDDMM (out) and its gradient kernel (y = sum_e rhs[e,h] v[col_e]);
+      * the edge softmax: weights in [0, 1], each row's weights sum to 1, sampled rows against
+        a float64 softmax of the scores (mean over heads, model.py:4270-4275);
+      * the segmented max equals the max over each sampled row's scores; same bits twice."""
+    from igr import ops
+    from igr.dataset import synthetic_pairs
+    from igr.dist_train import FeatureShard
+    U, I, E, d, H = 10_000_000, 1_000_000, 200_000_000, 64, 4
+    pairs = synthetic_pairs(U, I, E, 0)
+    g = FeatureShard(pairs, U, I, 0, U, 0, DEV).graph
+    del pairs
+    assert g.nnz == 410_995_952
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    u = torch.randn(g.n_rows, H * d, device=DEV, generator=gen) * 0.1
+    v = torch.randn(g.n_cols, d, device=DEV, generator=gen) * 0.1
+    out = ops.sddmm_shared(g, u, v, H)
+    assert torch.equal(out, ops.sddmm_shared(g, u, v, H))
+    hst = g.host()
+    rp, ci = hst['row_ptr'], hst['col_idx']
+    eid = hst['edge_id']
+    rng = np.random.default_rng(1)
+    rows = rng.integers(0, g.n_rows, 300)
+    for r in rows:
+        b, e = int(rp[r]), int(rp[r + 1])
+        if b == e:
+            continue
+        ids = torch.from_numpy((eid[b:e] if eid is not None else np.arange(b, e)).astype(np.int64)).to(DEV)
+        vc = v[torch.from_numpy(ci[b:e].astype(np.int64)).to(DEV)].double()       # [deg, d]
+        ref = torch.einsum('hd,ed->eh', u[r].double().view(H, d), vc)               # [deg, H]
+        got = out[ids].double()
+        assert float((got - ref).abs().max()) <= 1e-5 * float(ref.abs().max()) + 1e-7
+        # the segmented max over this row's scores
+    smax = ops.segment_reduce(g, out, 'max')
+    for r in rows[:100]:
+        b, e = int(rp[r]), int(rp[r + 1])
+        if b == e:
+            continue
+        ids = torch.from_numpy((eid[b:e] if eid is not None else np.arange(b, e)).astype(np.int64)).to(DEV)
+        assert torch.equal(smax[r], out[ids].max(0).values)
+    # adjoint identity with the gradient kernel
+    rhs = torch.randn(g.nnz, H, device=DEV, generator=gen)
+    y = ops.spmm_shared_heads(g, v, rhs, H)
+    lhs = float((u.double() * y.double()).sum())
+    rsum_ = float((rhs.double() * out.double()).sum())
+    scale = float((rhs.double().abs() * out.double().abs()).sum())
+    assert abs(lhs - rsum_) <= 1e-6 * scale
+    del rhs, y
+    # edge softmax (mean over heads of the per-head row softmax of out / sqrt(d) / 10)
+    w, rmax, rsum = ops.att_softmax(g, out, ops.sqrt_scale(d))
+    assert float(w.min()) >= 0.0 and float(w.max()) <= 1.0 + 1e-6
+    tot = ops.segment_reduce(g, w, 'sum')
+    deg = torch.from_numpy(np.diff(rp)).to(DEV)
+    assert float((tot[deg > 0] - 1.0).abs().max()) <= 1e-5
+    for r in rows[:100]:
+        b, e = int(rp[r]), int(rp[r + 1])
+        if b == e:
+            continue
+        ids = torch.from_numpy((eid[b:e] if eid is not None else np.arange(b, e)).astype(np.int64)).to(DEV)
+        ref = torch.softmax(out[ids].double() / float(np.float32(np.sqrt(d))) / 10., 0).mean(1)
+        assert float((w[ids].double() - ref).abs().max()) <= 3e-6
 
 
 # ---------------------------------------------------------------- items outnumber users, items sharded (world 2)

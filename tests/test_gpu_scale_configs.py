@@ -330,6 +330,50 @@ def test_attention_kernels_full_size_properties():
         assert float((w[ids].double() - ref).abs().max()) <= 3e-6
 
 
+@pytest.mark.parametrize('mode', ['eval', 'train'])
+def test_igcn_forward_backward_adjoint_at_training_scale(mode):
+    """IGCN's get_rep is linear in the embedding table (model.py:4188-4200: rep = P E, P the
+    layer mean of powers of A applied to the inductive layer F), so its backward must be the
+    transpose: <G, P E> = <P^T G, E>.  On a 1 M x 100 K x 20 M-draw graph (d = 64, L = 3), in
+    eval mode and in train mode, where the forward and the reverse feature SpMM have to draw
+    the same in-kernel dropout mask (model.py:4189, 4019-4028) for the identity to hold.
+    Also: the row-restricted path (last layer only at a batch's rows) equals those rows of
+    the full rep."""
+    from igr import ops
+    from igr.dataset import synthetic_pairs
+    U, I, E, d = 1_000_000, 100_000, 20_000_000, 64
+    pairs = synthetic_pairs(U, I, E, 0)
+
+    class Data:
+        name = 'synthetic'
+        n_users, n_items, train_pairs = U, I, pairs
+        train_array = pairs
+        train_data = None
+
+        def __len__(self):
+            return len(pairs)
+    torch.manual_seed(0)
+    m = M.IGCN({'name': 'IGCN', 'embedding_size': d, 'n_layers': 3, 'device': DEV, 'dropout': 0.3,
+                'feature_ratio': 1., 'dataset': Data(), 'batch_rep': False})
+    m.train(mode == 'train')
+    gen = torch.Generator(device=DEV).manual_seed(7)
+    G = torch.randn(U + I, d, device=DEV, generator=gen)
+    rep = m.get_rep()
+    (rep * G).sum().backward()
+    emb = m.embedding.weight
+    lhs = float((G.double() * rep.detach().double()).sum())
+    rhs = float((emb.grad.double() * emb.detach().double()).sum())
+    scale = float((G.double().abs() * rep.detach().double().abs()).sum())
+    assert abs(lhs - rhs) <= 2e-6 * scale, (lhs, rhs, scale)
+    if mode == 'eval':
+        with torch.no_grad():
+            rows = torch.randint(0, U + I, (6144,), device=DEV, generator=gen)
+            rb = ops.propagate_rows(m.norm_adj, emb, m.n_layers, rows, feat=m.feat_mat, fvals=m.inductive_values(),
+                                    adj_vals=m.norm_vals)
+            ref = rep.detach()[rows]
+            assert float((rb - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
+
+
 # ---------------------------------------------------------------- items outnumber users, items sharded (world 2)
 
 AM_U, AM_I, AM_E, AM_D = 52_000, 290_000, 3_000_000, 128

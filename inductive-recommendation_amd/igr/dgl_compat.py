@@ -9,7 +9,8 @@ The reference reaches its graph arithmetic through exactly two DGL entry points
 
 so replacing that import with `import igr.dgl_compat as dgl` moves those call
 sites onto the HIP kernels with no other edit: same argument names, same
-autograd behaviour (gradients with respect to lhs_data and rhs_data), errors
+autograd behaviour (gradients with respect to lhs_data and rhs_data; the max
+reduction sends each row's gradient to its arg-max edge, as DGL's does), errors
 raised as exceptions.  `gsddmm(g, 'dot', lhs, rhs, h)` is offered beside them for
 the masked per-edge dot product the reference writes by hand (model.py:4246-4255).
 """

@@ -536,6 +536,37 @@ class SegmentSum(torch.autograd.Function):
         return None, dx if dout.dim() == 2 else dx[:, 0]
 
 
+class SegmentMax(torch.autograd.Function):
+    """gspmm(g, 'copy_rhs', 'max', None, x) with DGL's backward: each row's gradient goes to
+    the edge that holds the row's maximum (the first one in edge order on ties, as a
+    compare-greater scan over the row finds it).  The API-compatible path of model.py:4270;
+    the fused edge softmax (AttSoftmax) needs no such gradient."""
+
+    @staticmethod
+    def forward(ctx, g, x):
+        out = segment_reduce(g, x, 'max')
+        ctx.g = g
+        ctx.save_for_backward(x, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, out = ctx.saved_tensors
+        g = ctx.g
+        rows = g.edge_rows()
+        x2 = x if x.dim() == 2 else x[:, None]
+        o2 = out if out.dim() == 2 else out[:, None]
+        d2 = dout if dout.dim() == 2 else dout[:, None]
+        is_max = x2 == o2[rows]
+        nnz = x2.shape[0]
+        idx = torch.arange(nnz, device=x.device)[:, None].expand_as(x2)
+        cand = torch.where(is_max, idx, torch.full_like(idx, nnz))
+        first = torch.full(o2.shape, nnz, dtype=idx.dtype, device=x.device)
+        first = first.scatter_reduce(0, rows[:, None].expand_as(x2), cand, 'amin')
+        dx = torch.where(cand == first[rows], d2[rows], torch.zeros((), dtype=d2.dtype, device=x.device))
+        return None, dx if x.dim() == 2 else dx[:, 0]
+
+
 class AttSoftmax(torch.autograd.Function):
     """AttIGCN edge softmax + head mean (model.py:4270-4275); `keep` marks the
     edges present after dropout (keep == 0: removed, as dropout_sp_mat does)."""
@@ -975,7 +1006,7 @@ def gspmm(g, op, reduce_op, lhs_data, rhs_data):
         return SegmentSum.apply(g, rhs_data)
     if op == 'copy_rhs' and reduce_op == 'max':
         if rhs_data.requires_grad and torch.is_grad_enabled():
-            raise IgrError('gspmm copy_rhs/max backward is not provided; detach the input')
+            return SegmentMax.apply(g, rhs_data)
         return segment_reduce(g, rhs_data, 'max')
     raise IgrError(f'gspmm op ({op}, {reduce_op}) not supported')
 

@@ -389,6 +389,20 @@ int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int64_t lda, i
                  const float *b, int64_t ldb, int32_t trans_b, const float *bias, float *c,
                  int64_t ldc, void *workspace, int64_t ws_bytes, void *stream);
 
+/* Weight and bias gradients of a Linear applied to every node (the backward of NGCF's
+ * Linear(d, d), model.py:4039, and AttIGCN's Linear(d, 4d), model.py:4259, 4264, under
+ * loss.backward(), trainer.py:553):
+ *   dw[n, c] = sum_m dy[m, n] * x[m, c]   (n < n_out, c < k_in),   db[n] = sum_m dy[m, n]
+ * streamed over the m node rows with the dW block held in MFMA accumulators; partial
+ * blocks of row ranges go to `workspace` (igr_linear_wgrad_workspace_size bytes, 16-byte
+ * aligned) and are added in range order (the same bits on every run).  db nullable.
+ * Supported: k_in in {32, 64}, n_out in {64, 128} or a multiple of 256, dy / x 16-byte
+ * aligned with leading dimensions a multiple of 4; other shapes: igr_gemm_f32 (trans_a). */
+int64_t igr_linear_wgrad_workspace_size(int64_t m, int32_t n_out, int32_t k_in);
+int igr_linear_wgrad_f32(int64_t m, int32_t n_out, int32_t k_in, const float *dy, int64_t ld_dy, const float *x,
+                         int64_t ld_x, float *dw, int64_t ld_dw, float *db, void *workspace, int64_t ws_bytes,
+                         void *stream);
+
 /* ------------------------------------------------------- training step */
 
 /* Device-side BPR sampler (dataset.py:119-131 semantics):

@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, 'csrc')
 INCLUDE = os.path.join(ROOT, 'include')
 OBJ = os.path.join(HERE, 'build')
 LIB = os.path.join(HERE, 'igr', 'lib', 'libigr.so')
-SOURCES = ['spmm.hip', 'spmm_rows.hip', 'topk.hip', 'edge_ops.hip', 'att_shared.hip', 'bpr.hip', 'rowsort.hip', 'gemm.hip', 'train_ops.hip', 'graph_host.cpp', 'capi.cpp']
+SOURCES = ['spmm.hip', 'spmm_rows.hip', 'topk.hip', 'edge_ops.hip', 'att_shared.hip', 'bpr.hip', 'rowsort.hip', 'gemm.hip', 'linear_wgrad.hip', 'train_ops.hip', 'graph_host.cpp', 'capi.cpp']
 ARCH = os.environ.get('IGR_OFFLOAD_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 # Packed fp32 VALU ops are switched off for the device pass (some of their

@@ -96,6 +96,9 @@ SIGNATURES = {
     'igr_adam_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,
                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i64, c_vp, c_vp]),
     'igr_counter_add': (ctypes.c_int, [c_vp, c_i64, c_vp]),
+    'igr_linear_wgrad_workspace_size': (c_i64, [c_i64, c_i32, c_i32]),
+    'igr_linear_wgrad_f32': (ctypes.c_int, [c_i64, c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64,
+                                            c_vp]),
     'igr_means_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     'igr_loss_combine_f32': (ctypes.c_int, [c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_vp, c_vp, c_vp]),
 }

@@ -452,6 +452,27 @@ def gemm(a, b, bias=None, trans_a=False, trans_b=False):
     return c
 
 
+def linear_wgrad(dy, x, want_db=True):
+    """(dW, db) of y = x W^T + b over all rows: dW = dy^T x, db = column sums of dy.  Shapes the
+    streamed kernel takes (igr_linear_wgrad_f32) get both from one pass over dy and x; others
+    get dW from the split-K GEMM and db = None (the caller sums)."""
+    _dev(dy, x)
+    dy, x = _f32(dy).contiguous(), _f32(x).contiguous()
+    m, n_out = dy.shape
+    k_in = x.shape[1]
+    if x.shape[0] != m:
+        raise IgrError(f'linear_wgrad: dy has {m} rows, x has {x.shape[0]}')
+    wsb = int(L.lib().igr_linear_wgrad_workspace_size(m, n_out, k_in))
+    if wsb <= 0 or dy.data_ptr() % 16 or x.data_ptr() % 16:
+        return gemm(dy, x, trans_a=True, trans_b=True), None
+    ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=dy.device)
+    dw = torch.empty(n_out, k_in, dtype=torch.float32, device=dy.device)
+    db = torch.empty(n_out, dtype=torch.float32, device=dy.device) if want_db else None
+    L.call('igr_linear_wgrad_f32', m, n_out, k_in, _p(dy), dy.stride(0), _p(x), x.stride(0), _p(dw), k_in, _p(db),
+           _p(ws), wsb, _stream())
+    return dw, db
+
+
 # ------------------------------------------------------------------ autograd
 
 class GSpMMSum(torch.autograd.Function):
@@ -598,8 +619,12 @@ class Linear(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         dy = dy.contiguous()
         dx = gemm(dy, weight, trans_b=True) if ctx.needs_input_grad[0] else None
-        dw = gemm(dy, x, trans_a=True, trans_b=True) if ctx.needs_input_grad[1] else None
-        db = dy.sum(0) if (ctx.has_bias and ctx.needs_input_grad[2]) else None
+        want_db = ctx.has_bias and ctx.needs_input_grad[2]
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            dw, db = linear_wgrad(dy, x, want_db)   # one streamed pass gives both when the shape allows
+        if want_db and db is None:
+            db = dy.sum(0)
         return dx, dw, db
 
 

@@ -14,7 +14,13 @@ VARIANTS = {
     'p_pin0': '-DIGR_GEMMP_PIN=0',                          # nothing may cross a store
     # diagnostics: what it costs to store C / load A
     'p_nostore': '-DIGR_GEMMP_NOSTORE',
+    # k steps per load group of the streamed weight-gradient kernel
+    'wg_pf4_w2048': '-DIGR_WGRAD_PF=4 -DIGR_WGRAD_OCC=2 -DIGR_WGRAD_WAVES=2048',
+    'wg_pf12_w1024': '-DIGR_WGRAD_PF=12',
 }
+# the streamed Linear weight / bias gradient (m, n_out, k_in): timed next to the split-K GEMM + column sum it replaces
+WGRAD = {'wgrad_att_ml1m': (9748, 256, 64), 'wgrad_att_1m': (1_100_002, 256, 64), 'wgrad_ngcf_1m': (1_100_000, 64, 64),
+         'wgrad_att_11m': (11_000_002, 256, 64)}
 ONLY = os.environ.get('IGR_TUNE_SHAPES')
 # name: (m, n, k, trans_a, trans_b)
 SHAPES = {
@@ -73,6 +79,33 @@ def one(name):
         err = float(((c.double() - ref).abs().max() / ref.abs().max()).item())
         res[sh] = {'us': us, 'cold_us': float(np.median(cold)), 'tflops': 2 * m * n * k / us / 1e6, 'max_rel_err': err}
         del a, b, c, ref
+        torch.cuda.empty_cache()
+    for sh, (m, n, k) in WGRAD.items():
+        if ONLY and sh not in ONLY.split(','):
+            continue
+        dy = torch.randn(m, n, device=dev)
+        x = torch.randn(m, k, device=dev)
+
+        def run(fn, cnt):
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(cnt)]
+            for e0, e1 in ev:
+                e0.record()
+                fn()
+                e1.record()
+            torch.cuda.synchronize()
+            return float(np.median([e0.elapsed_time(e1) * 1e3 for e0, e1 in ev]))
+        old = lambda: (ops.gemm(dy, x, trans_a=True, trans_b=True), dy.sum(0))  # noqa: E731
+        new = lambda: ops.linear_wgrad(dy, x)  # noqa: E731
+        out = {}
+        for name_, fn in (('gemm_plus_sum_us', old), ('streamed_us', new)):
+            run(fn, 10)
+            run(fn, int(min(500, max(10, 100e3 / max(run(fn, 5), 1.0)))))
+            out[name_] = run(fn, 30)
+        out['bytes'] = 4 * m * (n + k)
+        out['streamed_GBps'] = out['bytes'] / out['streamed_us'] / 1e3
+        out['streamed_tflops'] = 2 * m * n * k / out['streamed_us'] / 1e6
+        res[sh] = out
+        del dy, x
         torch.cuda.empty_cache()
     print(json.dumps(res), flush=True)
 

@@ -216,6 +216,10 @@ def test_new_entry_points_validate_arguments():
     # hipGraph-step entry points: the device counter, Adam's host step without one, per-head SpMM
     _refused('igr_counter_add', None, 1, st, match='NULL')
     _refused('igr_means_f32', 0, F, None, F, st, match='n <= 0')
+    assert _lib.lib().igr_linear_wgrad_workspace_size(1000, 192, 64) == 0      # 3 blocks of 64: the GEMM takes it
+    assert _lib.lib().igr_linear_wgrad_workspace_size(1_100_002, 256, 64) == 256 * 256 * 65 * 4   # 1024 waves / 4 blocks
+    _refused('igr_linear_wgrad_f32', 1000, 100, 64, F, 100, F, 64, F, 64, None, F, 1 << 20, st, match='supported')
+    _refused('igr_linear_wgrad_f32', 1000, 64, 64, F, 64, F, 64, F, 64, None, None, 0, st, match='workspace')
     _refused('igr_loss_combine_f32', None, None, None, 0.0, 0.0, 1.0, F, None, st, match='bpr')
     _refused('igr_adam_f32', 4, F, F, F, F, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None, st, match='step')
     _refused('igr_bpr_sample', 4, 0, F, F, F, 10, 1, 0, None, 8, F, F, F, st, match='active')

@@ -982,3 +982,38 @@ def test_loss_combine_is_the_reference_expression_bitwise():
         assert torch.equal(got, ref) and torch.equal(tot, ref_tot)
         assert torch.equal(ops.loss_combine(bpr, l2, None, c_l2), bpr + c_l2 * l2)   # BPRTrainer, trainer.py:424-425
         assert torch.equal(ops.loss_combine(bpr), bpr)
+
+
+@pytest.mark.parametrize('m,n_out,k_in', [(9748, 256, 64), (1000, 64, 64), (33001, 128, 32), (70, 64, 32), (31, 64, 64),
+                                          (4133, 512, 64), (20011, 64, 32), (1100002, 256, 64)])
+def test_linear_wgrad_streamed(m, n_out, k_in):
+    """dW = dy^T x and db = column sums of dy in one streamed pass (operands straight from
+    global memory into the MFMAs, partial blocks of row ranges added in order): against
+    float64, ranges with ragged ends, fewer rows than one group, the same bits twice, and the
+    autograd path of ops.linear."""
+    rng = np.random.default_rng(m + n_out + k_in)
+    dy = rng.standard_normal((m, n_out)).astype(np.float32)
+    x = rng.standard_normal((m, k_in)).astype(np.float32)
+    dw, db = ops.linear_wgrad(t(dy), t(x))
+    assert db is not None, 'the streamed kernel must take this shape'
+    ref_w = dy.astype(np.float64).T @ x.astype(np.float64)
+    ref_b = dy.astype(np.float64).sum(0)
+    scale = np.sqrt(m)
+    assert np.abs(dw.cpu().numpy() - ref_w).max() <= 2e-6 * scale * 4
+    assert np.abs(db.cpu().numpy() - ref_b).max() <= 2e-6 * scale * 4
+    dw2, db2 = ops.linear_wgrad(t(dy), t(x))
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    if m <= 40000:
+        lin = torch.nn.Linear(k_in, n_out).to(DEV)
+        xt = t(x)
+        (ops.linear(xt, lin) * t(dy)).sum().backward()
+        assert torch.equal(lin.weight.grad, dw) and torch.equal(lin.bias.grad, db)
+
+
+def test_linear_wgrad_other_shapes_take_the_gemm():
+    rng = np.random.default_rng(3)
+    dy = rng.standard_normal((500, 192)).astype(np.float32)
+    x = rng.standard_normal((500, 64)).astype(np.float32)
+    dw, db = ops.linear_wgrad(t(dy), t(x))
+    assert db is None
+    close(dw.cpu().numpy(), dy.astype(np.float64).T @ x.astype(np.float64), rtol=1e-5, atol_row=1e-5)

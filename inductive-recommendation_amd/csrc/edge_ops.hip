@@ -583,6 +583,11 @@ extern "C" int igr_sddmm_dot_f32(const igr_csr *g, int32_t h, int32_t d, const f
         if (!g || h <= 0 || d <= 0) return arg_error(fn, "bad graph / h / d");
         if (ld_u < (int64_t)h * d || ld_v < (int64_t)h * d) return arg_error(fn, "leading dimension < h*d");
         if (g->n_rows == 0 || g->nnz == 0) return IGR_OK;
+        // one head: the same sums as the shared-source kernel (one d-float source row per edge),
+        // whose gathers are unconditional and whose lane sums are DPP adds
+        if (h == 1 && (d == 32 || d == 64 || d == 128 || d == 256) && ld_u % 4 == 0 && ld_v % 4 == 0 &&
+            ld_v <= 2147483647 && aligned16(u) && aligned16(v))
+            return igr_sddmm_shared_f32(g, 1, d, u, ld_u, v, ld_v, out, stream);
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         const int64_t row_blocks = (g->n_rows + 3) / 4;
         const unsigned blocks = (unsigned)row_blocks;

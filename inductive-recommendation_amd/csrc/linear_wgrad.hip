@@ -170,27 +170,34 @@ __global__ __launch_bounds__(256, IGR_WGRAD_OCC) void linear_wgrad_kernel(int64_
     }
 }
 
-// dw[i] = sum_p part[p * nw + i] (i < nw) and db[j] = sum_p part_b[p * nb + j] (j < nb), p in
-// order; four independent chains per element keep loads in flight and are added in a fixed tree
-__global__ void wgrad_reduce_kernel(int64_t nw, int64_t nb, int64_t P, const float *__restrict__ part,
-                                    const float *__restrict__ part_b, float *__restrict__ dw, int64_t ld_dw, int cols,
-                                    float *__restrict__ db) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nw + nb) return;
+// dw[i] = sum_p part[p * nw + i] (i < nw) and db[j] = sum_p part_b[p * nb + j] (j < nb): 16
+// lanes per element, lane l adds partials l, l + 16, ... in order and the 16 lane sums are
+// added in a fixed xor tree - the same bits on every run.  (One thread per element walked
+// the workers serially: 12 us of dependent loads for 152 workers.)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(int64_t nw, int64_t nb, int64_t P,
+                                                           const float *__restrict__ part,
+                                                           const float *__restrict__ part_b, float *__restrict__ dw,
+                                                           int64_t ld_dw, int cols, float *__restrict__ db) {
+    const int l = threadIdx.x & 15;
+    int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    if (i >= nw + nb) return;  // whole 16-lane groups leave together
     const bool bias = i >= nw;
     const float *src = bias ? part_b : part;
     const int64_t n = bias ? nb : nw;
     if (bias) i -= nw;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int64_t p = 0;
-    for (; p + 3 < P; p += 4) {
+    float s0 = 0.f, s1 = 0.f;
+    int64_t p = l;
+    for (; p + 16 < P; p += 32) {
         s0 += src[p * n + i];
-        s1 += src[(p + 1) * n + i];
-        s2 += src[(p + 2) * n + i];
-        s3 += src[(p + 3) * n + i];
+        s1 += src[(p + 16) * n + i];
     }
-    for (; p < P; ++p) s0 += src[p * n + i];
-    const float v = (s0 + s1) + (s2 + s3);
+    if (p < P) s0 += src[p * n + i];
+    float v = s0 + s1;
+    v += shfl_xor_f(v, 8);
+    v += shfl_xor_f(v, 4);
+    v += shfl_xor_f(v, 2);
+    v += shfl_xor_f(v, 1);
+    if (l != 0) return;
     if (bias) {
         db[i] = v;
     } else {
@@ -249,7 +256,7 @@ extern "C" int igr_linear_wgrad_f32(int64_t m, int32_t n_out, int32_t k_in, cons
             hipLaunchKernelGGL((linear_wgrad_kernel<2>), grid, dim3(256), 0, st, m, (int)n_out, nb_in_wg, dy, ld_dy, x,
                                ld_x, ranges, part, part_b);
         const int64_t nw = (int64_t)n_out * k_in, nbias = db ? n_out : 0;
-        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nw + nbias + 255) / 256)), dim3(256), 0, st, nw, nbias,
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nw + nbias + 15) / 16)), dim3(256), 0, st, nw, nbias,
                            ranges, part, part_b, dw, ld_dw, (int)k_in, db);
         return launch_status(fn);
     });

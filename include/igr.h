@@ -441,6 +441,22 @@ int igr_means_f32(int64_t n, const float *a, const float *b, float *out, void *s
 int igr_loss_combine_f32(const float *bpr, const float *l2, const float *aux, float c_l2, float c_aux,
                          float weight, float *loss, float *loss_sum, void *stream);
 
+/* The same update for up to IGR_ADAM_MAX_SLOTS small tensors in one launch (projection
+ * weights, biases, feature weights: the optimizer's loop over parameters, trainer.py:44-46,
+ * 555).  `slots` is a host array; each slot's `step` is its own 1-based step count (added to
+ * *step_dev when given, as in igr_adam_f32).  Bit-identical to igr_adam_f32 per tensor. */
+#define IGR_ADAM_MAX_SLOTS 16
+typedef struct igr_adam_slot {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    int64_t n;
+    int64_t step;
+} igr_adam_slot;
+int igr_adam_multi_f32(int32_t n_slots, const igr_adam_slot *slots, double lr, double beta1, double beta2,
+                       double eps, double weight_decay, const int64_t *step_dev, void *stream);
+
 /* *counter += value on the stream (one device int64: the step counter a
  * captured training step advances at its end). */
 int igr_counter_add(int64_t *counter, int64_t value, void *stream);

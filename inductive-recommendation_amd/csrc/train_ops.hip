@@ -143,6 +143,65 @@ __global__ void adam_kernel(int64_t n, float *__restrict__ p, const float *__res
     }
 }
 
+// The same update for up to IGR_ADAM_MAX_SLOTS small tensors in ONE launch (a model's
+// projection weights, biases and feature weights: a launch each costs more than their
+// arithmetic).  Workgroup b serves 1024 elements of the slot whose block range holds b;
+// the arithmetic is adam_kernel's, expression for expression, so the bits are the same.
+struct AdamMulti {
+    float *p[IGR_ADAM_MAX_SLOTS];
+    const float *g[IGR_ADAM_MAX_SLOTS];
+    float *m[IGR_ADAM_MAX_SLOTS];
+    float *v[IGR_ADAM_MAX_SLOTS];
+    int64_t n[IGR_ADAM_MAX_SLOTS];
+    int64_t step0[IGR_ADAM_MAX_SLOTS];
+    float step_size[IGR_ADAM_MAX_SLOTS];
+    float bc2_sqrt[IGR_ADAM_MAX_SLOTS];
+    int32_t blk0[IGR_ADAM_MAX_SLOTS + 1];
+};
+
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a, int n_slots, float omb1, float b2, float omb2,
+                                                         float eps, float wd, const int64_t *__restrict__ step_dev,
+                                                         double lr, double beta1, double beta2) {
+    int k = 0;
+    while (k + 1 < n_slots && (int)blockIdx.x >= a.blk0[k + 1]) ++k;
+    float step_size = a.step_size[k], bc2_sqrt = a.bc2_sqrt[k];
+    if (step_dev) {
+        const double t = (double)(a.step0[k] + *step_dev);
+        step_size = (float)(lr / (1.0 - pow(beta1, t)));
+        bc2_sqrt = (float)sqrt(1.0 - pow(beta2, t));
+    }
+    float *__restrict__ p = a.p[k];
+    const float *__restrict__ g = a.g[k];
+    float *__restrict__ m = a.m[k];
+    float *__restrict__ v = a.v[k];
+    const int64_t n = a.n[k], n4 = n >> 2;
+    const int64_t i = (int64_t)((int)blockIdx.x - a.blk0[k]) * 256 + threadIdx.x;  // float4 index
+    if (i < n4) {
+        float4 pp = reinterpret_cast<float4 *>(p)[i], gg = reinterpret_cast<const float4 *>(g)[i];
+        float4 mm = reinterpret_cast<float4 *>(m)[i], vv = reinterpret_cast<float4 *>(v)[i];
+        float *pa = &pp.x, *ga = &gg.x, *ma = &mm.x, *va = &vv.x;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float gk = wd != 0.f ? ga[q] + wd * pa[q] : ga[q];
+            ma[q] = ma[q] + omb1 * (gk - ma[q]);
+            va[q] = va[q] * b2 + omb2 * gk * gk;
+            const float den = sqrtf(va[q]) / bc2_sqrt + eps;
+            pa[q] = pa[q] - step_size * (ma[q] / den);
+        }
+        reinterpret_cast<float4 *>(p)[i] = pp;
+        reinterpret_cast<float4 *>(m)[i] = mm;
+        reinterpret_cast<float4 *>(v)[i] = vv;
+    }
+    // the last n % 4 elements: the slot's first workgroup
+    const int64_t j = 4 * n4 + threadIdx.x;
+    if ((int)blockIdx.x == a.blk0[k] && j < n) {
+        const float gk = wd != 0.f ? g[j] + wd * p[j] : g[j];
+        m[j] = m[j] + omb1 * (gk - m[j]);
+        v[j] = v[j] * b2 + omb2 * gk * gk;
+        p[j] = p[j] - step_size * (m[j] / (sqrtf(v[j]) / bc2_sqrt + eps));
+    }
+}
+
 static unsigned grid_for(int64_t n, int block) {
     int64_t g = (n + block - 1) / block;
     if (g > 16384) g = 16384;
@@ -209,6 +268,39 @@ extern "C" int igr_adam_f32(int64_t n, float *param, const float *grad, float *e
         else IGR_ADAM(1);
 #undef IGR_ADAM
         return launch_status("igr_adam_f32");
+    });
+}
+
+extern "C" int igr_adam_multi_f32(int32_t n_slots, const igr_adam_slot *slots, double lr, double beta1, double beta2,
+                                  double eps, double weight_decay, const int64_t *step_dev, void *stream) {
+    return guarded("igr_adam_multi_f32", [&]() -> int {
+        const char *fn = "igr_adam_multi_f32";
+        if (n_slots < 0 || n_slots > IGR_ADAM_MAX_SLOTS) return arg_error(fn, "0 <= n_slots <= IGR_ADAM_MAX_SLOTS");
+        if (n_slots == 0) return IGR_OK;
+        if (!slots) return arg_error(fn, "NULL slots");
+        AdamMulti a;
+        int64_t blocks = 0;
+        for (int k = 0; k < n_slots; ++k) {
+            const igr_adam_slot &s = slots[k];
+            if (s.n <= 0 || s.n > (int64_t(1) << 30)) return arg_error(fn, "slot size must be in (0, 2^30]");
+            if (s.step < (step_dev ? 0 : 1)) return arg_error(fn, "step must be >= 1");
+            if (!s.param || !s.grad || !s.exp_avg || !s.exp_avg_sq) return arg_error(fn, "NULL pointer in a slot");
+            if (!aligned16(s.param) || !aligned16(s.grad) || !aligned16(s.exp_avg) || !aligned16(s.exp_avg_sq))
+                return arg_error(fn, "buffers must be 16-byte aligned");
+            const double bc1 = step_dev ? 1.0 : 1.0 - std::pow(beta1, (double)s.step);
+            const double bc2 = step_dev ? 1.0 : 1.0 - std::pow(beta2, (double)s.step);
+            a.p[k] = s.param, a.g[k] = s.grad, a.m[k] = s.exp_avg, a.v[k] = s.exp_avg_sq;
+            a.n[k] = s.n, a.step0[k] = s.step;
+            a.step_size[k] = (float)(lr / bc1), a.bc2_sqrt[k] = (float)std::sqrt(bc2);
+            a.blk0[k] = (int32_t)blocks;
+            blocks += std::max<int64_t>(1, ((s.n >> 2) + 255) / 256);
+            if (blocks > 2147483647) return arg_error(fn, "too many elements for one launch");
+        }
+        a.blk0[n_slots] = (int32_t)blocks;
+        hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                           a, (int)n_slots, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
+                           (float)weight_decay, step_dev, lr, beta1, beta2);
+        return launch_status(fn);
     });
 }
 

@@ -30,6 +30,13 @@ class IgrCsr(ctypes.Structure):
     ]
 
 
+ADAM_MAX_SLOTS = 16
+
+
+class IgrAdamSlot(ctypes.Structure):          # struct igr_adam_slot
+    _fields_ = [('param', c_vp), ('grad', c_vp), ('exp_avg', c_vp), ('exp_avg_sq', c_vp), ('n', c_i64), ('step', c_i64)]
+
+
 class IgrEpilogue(ctypes.Structure):
     """struct igr_epilogue (include/igr.h)."""
     _fields_ = [
@@ -95,6 +102,8 @@ SIGNATURES = {
                                       c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     'igr_adam_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,
                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i64, c_vp, c_vp]),
+    'igr_adam_multi_f32': (ctypes.c_int, [c_i32, c_vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                          ctypes.c_double, ctypes.c_double, c_vp, c_vp]),
     'igr_counter_add': (ctypes.c_int, [c_vp, c_i64, c_vp]),
     'igr_linear_wgrad_workspace_size': (c_i64, [c_i64, c_i32, c_i32]),
     'igr_linear_wgrad_f32': (ctypes.c_int, [c_i64, c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64,

@@ -215,6 +215,8 @@ def test_new_entry_points_validate_arguments():
     _refused('igr_dropout_uniforms', None, 1, 0, None, 0, F, st, match='NULL')
     # hipGraph-step entry points: the device counter, Adam's host step without one, per-head SpMM
     _refused('igr_counter_add', None, 1, st, match='NULL')
+    _refused('igr_adam_multi_f32', 17, F, 1e-3, 0.9, 0.999, 1e-8, 0.0, None, st, match='n_slots')
+    _refused('igr_adam_multi_f32', 1, None, 1e-3, 0.9, 0.999, 1e-8, 0.0, None, st, match='NULL')
     _refused('igr_means_f32', 0, F, None, F, st, match='n <= 0')
     assert _lib.lib().igr_linear_wgrad_workspace_size(1000, 192, 64) == 0      # 3 blocks of 64: the GEMM takes it
     assert _lib.lib().igr_linear_wgrad_workspace_size(1_100_002, 256, 64) == 256 * 256 * 65 * 4   # 1024 waves / 4 blocks

@@ -1017,3 +1017,52 @@ def test_linear_wgrad_other_shapes_take_the_gemm():
     dw, db = ops.linear_wgrad(t(dy), t(x))
     assert db is None
     close(dw.cpu().numpy(), dy.astype(np.float64).T @ x.astype(np.float64), rtol=1e-5, atol_row=1e-5)
+
+
+def test_fused_adam_small_tensors_share_one_launch():
+    """A model's small parameters (projection weights, biases, feature weights) go through
+    igr_adam_multi_f32 in one launch: bit-identical to the per-tensor kernel, sizes that are
+    not multiples of 4 or of a workgroup, more tensors than one launch holds, a device step
+    counter; and the torch.optim.Adam rule to rounding."""
+    from igr import optim
+    rng = np.random.default_rng(21)
+    sizes = [1, 3, 64, 255, 1024, 1025, 256 * 64, 70001] + [5] * 14   # 22 tensors: two launches
+    init = [rng.standard_normal(n).astype(np.float32) for n in sizes]
+    grads = [[rng.standard_normal(n).astype(np.float32) for n in sizes] for _ in range(4)]
+
+    def run(small_numel, ctr=None):
+        keep = optim.SMALL_NUMEL
+        optim.SMALL_NUMEL = small_numel
+        try:
+            ps = [t(a).requires_grad_(True) for a in init]
+            opt = optim.Adam(ps, lr=1e-2, weight_decay=1e-3)
+            if ctr is not None:
+                opt.set_device_step(ctr)
+            for gs in grads:
+                for p, g in zip(ps, gs):
+                    p.grad = t(g)
+                opt.step()
+                if ctr is not None:
+                    ctr.add_(1)
+            return ps, opt
+        finally:
+            optim.SMALL_NUMEL = keep
+    multi, om = run(1 << 18)
+    single, os_ = run(0)
+    for a, b in zip(multi, single):
+        assert torch.equal(a, b)
+        assert torch.equal(om.state[a]['exp_avg'], os_.state[b]['exp_avg'])
+        assert torch.equal(om.state[a]['exp_avg_sq'], os_.state[b]['exp_avg_sq'])
+    dev_multi, _ = run(1 << 18, torch.zeros(1, dtype=torch.int64, device=DEV))
+    dev_single, _ = run(0, torch.zeros(1, dtype=torch.int64, device=DEV))
+    for a, b, c in zip(dev_multi, dev_single, multi):
+        assert torch.equal(a, b)
+        np.testing.assert_allclose(a.detach().cpu().numpy(), c.detach().cpu().numpy(), rtol=2e-6, atol=2e-7)
+    ref = [t(a).requires_grad_(True) for a in init]
+    ot = torch.optim.Adam(ref, lr=1e-2, weight_decay=1e-3)
+    for gs in grads:
+        for p, g in zip(ref, gs):
+            p.grad = t(g)
+        ot.step()
+    for a, b in zip(multi, ref):
+        np.testing.assert_allclose(a.detach().cpu().numpy(), b.detach().cpu().numpy(), rtol=2e-6, atol=2e-7)

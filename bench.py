@@ -218,6 +218,9 @@ def main():
         if done is not None:
             done.record(stream)  # after the compute stream's wait on the last all-reduces
 
+    # one priming step outside the W warm-up steps: the first call of each kernel loads its code
+    # object and allocates the split-row workspaces (16.8 ms against 15.3 ms for a steady step)
+    step()
     for _ in range(args.warmup):
         step()
     drain()

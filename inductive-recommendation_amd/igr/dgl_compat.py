@@ -22,7 +22,7 @@ import torch
 from . import ops as _ops
 
 _CACHE = collections.OrderedDict()
-_CACHE_SIZE = 8
+_CACHE_SIZE = 4  # each entry pins a CSR and its launch plan in HBM
 
 
 def graph(edges, num_nodes=None, device='cuda'):

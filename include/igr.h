@@ -286,6 +286,12 @@ int igr_topk_f32(int64_t n_rows, int64_t n_cols, const float *scores, int64_t ld
 int igr_dropout_uniforms(const igr_csr *g, uint64_t seed, uint64_t offset, const int64_t *offset_dev,
                          int32_t transposed, float *out, void *stream);
 
+/* igr_edge_dropout_f32 with those uniforms drawn in the same pass (no rand array):
+ * out[e] = val[e] / (1 - p) where floor((1 - p) + U_e) is 1, else 0, e by edge id
+ * (NGCF.dropout_sp_mat, model.py:4016-4028, as a value mask over the fixed CSR). */
+int igr_edge_dropout_counter_f32(const igr_csr *g, const float *val, float p, uint64_t seed, uint64_t offset,
+                                 const int64_t *offset_dev, int32_t transposed, float *out, void *stream);
+
 /* u_dot_v SDDMM: out[eid(p), h] = <u[row_p, h, :], v[col_p, h, :]>.
  * AttIGCN.masked_mm (model.py:4246-4255) with u = x_q (dst rows),
  * v = x_k (src rows); with h = 1 it is also the gspmm rhs-gradient.

@@ -524,16 +524,26 @@ static int run_spmm(const char *fn, const igr_csr *g, int32_t d, const float *x,
 
 // The uniforms W_Scaled draws, per CSR position of g (explicit-values path:
 // AttIGCN's per-edge dropout; tests).  One wave per row, lanes over its edges.
+// With val: the dropout itself in the same pass, by edge id - out[e] = val[e] / keep where
+// floor(keep + U) is 1, else 0 (model.py:4019-4027), the expression of edge_dropout_kernel.
 __global__ __launch_bounds__(256) void uniforms_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr,
-                                                       const int32_t *__restrict__ col, uint64_t seed, uint64_t offset,
+                                                       const int32_t *__restrict__ col,
+                                                       const int64_t *__restrict__ eid, uint64_t seed, uint64_t offset,
                                                        const int64_t *__restrict__ offset_dev, int swap,
+                                                       const float *__restrict__ val, float keep,
                                                        float *__restrict__ out) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n_rows) return;
     const uint64_t off = offset + (offset_dev ? (uint64_t)*offset_dev : 0);
     for (int64_t p = row_ptr[r] + (threadIdx.x & 63); p < row_ptr[r + 1]; p += 64) {
         const uint32_t c = (uint32_t)col[p];
-        out[p] = uniform24(seed, off, swap ? edge_key(c, (uint32_t)r) : edge_key((uint32_t)r, c));
+        const float u = uniform24(seed, off, swap ? edge_key(c, (uint32_t)r) : edge_key((uint32_t)r, c));
+        if (!val) {
+            out[p] = u;
+        } else {
+            const int64_t e = eid ? eid[p] : p;
+            out[e] = floorf(keep + u) != 0.f ? val[e] / keep : 0.f;
+        }
     }
 }
 
@@ -663,7 +673,25 @@ extern "C" int igr_dropout_uniforms(const igr_csr *g, uint64_t seed, uint64_t of
         if (g->n_rows > 4294967295LL || g->n_cols > 4294967295LL)
             return arg_error("igr_dropout_uniforms", "dropout keys need row / column ids below 2^32");
         hipLaunchKernelGGL(uniforms_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0, st, g->n_rows,
-                           g->row_ptr, g->col_idx, seed, offset, offset_dev, transposed ? 1 : 0, out);
+                           g->row_ptr, g->col_idx, g->edge_id, seed, offset, offset_dev, transposed ? 1 : 0,
+                           (const float *)nullptr, 1.f, out);
         return launch_status("igr_dropout_uniforms");
+    });
+}
+
+extern "C" int igr_edge_dropout_counter_f32(const igr_csr *g, const float *val, float p, uint64_t seed, uint64_t offset,
+                                            const int64_t *offset_dev, int32_t transposed, float *out, void *stream) {
+    return guarded("igr_edge_dropout_counter_f32", [&]() -> int {
+        const char *fn = "igr_edge_dropout_counter_f32";
+        if (!g || !val || !out) return arg_error(fn, "NULL pointer");
+        if (!(p >= 0.f && p < 1.f)) return arg_error(fn, "p must be in [0, 1)");
+        if (g->n_rows == 0 || g->nnz == 0) return IGR_OK;
+        if (g->n_rows > 4294967295LL || g->n_cols > 4294967295LL)
+            return arg_error(fn, "dropout keys need row / column ids below 2^32");
+        const float keep = (float)(1.0 - (double)p);
+        hipLaunchKernelGGL(uniforms_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0,
+                           reinterpret_cast<hipStream_t>(stream), g->n_rows, g->row_ptr, g->col_idx, g->edge_id, seed,
+                           offset, offset_dev, transposed ? 1 : 0, val, keep, out);
+        return launch_status(fn);
     });
 }

@@ -80,6 +80,8 @@ SIGNATURES = {
     'igr_mask_scores_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     'igr_topk_f32': (ctypes.c_int, [c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),
     'igr_dropout_uniforms': (ctypes.c_int, [_P(IgrCsr), ctypes.c_uint64, ctypes.c_uint64, c_vp, c_i32, c_vp, c_vp]),
+    'igr_edge_dropout_counter_f32': (ctypes.c_int, [_P(IgrCsr), c_vp, c_f32, ctypes.c_uint64, ctypes.c_uint64, c_vp,
+                                                    c_i32, c_vp, c_vp]),
     'igr_sddmm_dot_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     'igr_sddmm_shared_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     'igr_spmm_shared_heads_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),

@@ -248,7 +248,7 @@ def dropout_values(model, vals, graph=None):
         rand = torch.rand(n).to(vals.device)
     elif graph is not None:
         seed, step, ctr = model.next_dropout_step()
-        rand = ops.dropout_uniforms(graph, seed, step, offset_dev=ctr)
+        return ops.edge_dropout_counter(graph, vals, model.dropout, seed, step, offset_dev=ctr)
     else:
         rand = torch.rand(n, device=vals.device)
     return ops.edge_dropout(vals, rand, model.dropout)

@@ -331,6 +331,20 @@ def att_softmax_bwd(g: Graph, alpha, sqrt_d, rmax, rsum, dw, keep=None):
     return dalpha
 
 
+def edge_dropout_counter(g: Graph, val, p, seed, offset, swap=False, offset_dev=None, out=None):
+    """edge_dropout(val, dropout_uniforms(g, seed, offset, ...), p) in one pass, no rand array
+    (igr_edge_dropout_counter_f32); val and out by edge id."""
+    _dev(val, out, offset_dev)
+    val = _f32(val).contiguous()
+    if val.numel() != g.nnz:
+        raise IgrError(f'edge_dropout_counter: {val.numel()} values for {g.nnz} edges')
+    if out is None:
+        out = torch.empty_like(val)
+    L.call('igr_edge_dropout_counter_f32', ctypes.byref(g.csr), _p(val), float(p), ctypes.c_uint64(seed & (2 ** 64 - 1)),
+           ctypes.c_uint64(offset & (2 ** 64 - 1)), _p(offset_dev), int(swap), _p(out), _stream())
+    return out
+
+
 def edge_dropout(val, rand, p, out=None):
     _dev(val, rand, out)
     if rand.numel() != val.numel():

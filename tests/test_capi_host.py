@@ -213,6 +213,7 @@ def test_new_entry_points_validate_arguments():
         _refused('igr_spmm_scaled_f32', ctypes.byref(rect.csr), 64, F, 64, None, None, keep, 1, 0, None, 0, F, 64,
                  None, F, st, match='keep')
     _refused('igr_dropout_uniforms', None, 1, 0, None, 0, F, st, match='NULL')
+    _refused('igr_edge_dropout_counter_f32', ctypes.byref(rect.csr), F, 1.0, 1, 0, None, 0, F, st, match='p must')
     # hipGraph-step entry points: the device counter, Adam's host step without one, per-head SpMM
     _refused('igr_counter_add', None, 1, st, match='NULL')
     _refused('igr_adam_multi_f32', 17, F, 1e-3, 0.9, 0.999, 1e-8, 0.0, None, st, match='n_slots')

@@ -1066,3 +1066,26 @@ def test_fused_adam_small_tensors_share_one_launch():
         ot.step()
     for a, b in zip(multi, ref):
         np.testing.assert_allclose(a.detach().cpu().numpy(), b.detach().cpu().numpy(), rtol=2e-6, atol=2e-7)
+
+
+@pytest.mark.parametrize('dedup', [True, False])
+def test_edge_dropout_counter_equals_two_step_form(dedup):
+    """Dropout with the uniforms drawn in the same pass == edge_dropout(val, dropout_uniforms(...)):
+    the same bits, values addressed by edge id (a multigraph keeps edge ids != CSR positions),
+    a device step counter, the transposed key."""
+    g, _ = rand_graph(400, 300, 12000, seed=5, skew=True, dedup=dedup)
+    val = torch.rand(g.nnz, device=DEV) + 0.5
+    hst = g.host()
+    eid = hst['edge_id']
+    for swap in (False, True):
+        for ctr in (None, torch.tensor([7], dtype=torch.int64, device=DEV)):
+            u = ops.dropout_uniforms(g, 1234, 5, swap=swap, offset_dev=ctr)          # by CSR position
+            by_eid = torch.empty_like(u)
+            if eid is not None:
+                by_eid[torch.from_numpy(eid.astype(np.int64)).to(DEV)] = u
+            else:
+                by_eid = u
+            ref = ops.edge_dropout(val, by_eid, 0.3)
+            got = ops.edge_dropout_counter(g, val, 0.3, 1234, 5, swap=swap, offset_dev=ctr)
+            assert torch.equal(got, ref)
+            assert 0.2 < float((got == 0).float().mean()) < 0.4

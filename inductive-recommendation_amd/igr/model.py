@@ -414,8 +414,22 @@ class IGCN(BasicModel):
         On the row path the aux term rides in the same autograd node, so its
         gradient is added into the embedding gradient in place."""
         if not self._rows_path(users.numel()):
+            side = self._aux_stream()
+            if side is None:
+                bpr, l2 = self.bpr_loss(users, pos_items, neg_items, need_l2)
+                return bpr, l2, self.aux_loss(a_users, a_pos, a_neg)
+            # the aux term touches only the raw table: its forward (and, through autograd's stream
+            # bookkeeping, its backward) runs on a second stream beside the propagation
+            cur = torch.cuda.current_stream()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                for t in (a_users, a_pos, a_neg):
+                    t.record_stream(side)
+                aux = self.aux_loss(a_users, a_pos, a_neg)
             bpr, l2 = self.bpr_loss(users, pos_items, neg_items, need_l2)
-            return bpr, l2, self.aux_loss(a_users, a_pos, a_neg)
+            cur.wait_stream(side)
+            aux.record_stream(cur)
+            return bpr, l2, aux
         rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
         rep_b, aux = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
                                         feat=self.feat_mat, fvals=self.inductive_values(), adj_vals=self.norm_vals,
@@ -425,6 +439,24 @@ class IGCN(BasicModel):
             return bpr, None, aux
         extra = self._l2_extra()
         return bpr, (l2 if extra is None else l2 + extra), aux
+
+    def _aux_stream(self):
+        """The stream of the aux term inside a hipGraph-captured step (config 'aux_stream': True
+        forces it in eager steps too, False switches it off); default priority, as every stream
+        here.  In a captured step the two branches become independent graph nodes; an eager step
+        is bound by the host, which a second stream does not help."""
+        want = self.config.get('aux_stream', 'capture')
+        if want is False or not self.embedding.weight.is_cuda:
+            return None
+        if want == 'capture' and not torch.cuda.is_current_stream_capturing():
+            return None
+        if getattr(self, '_aux_side', None) is None:
+            self._aux_side = torch.cuda.Stream(device=self.embedding.weight.device)
+            # the table's gradient now arrives from two streams by design; autograd orders them
+            setter = getattr(torch.autograd.graph, 'set_warn_on_accumulate_grad_stream_mismatch', None)
+            if setter is not None:
+                setter(False)
+        return self._aux_side
 
     def aux_loss(self, users, pos_items, neg_items):
         """IGCNTrainer aux term (trainer.py:542-549) on the raw feature table with w."""

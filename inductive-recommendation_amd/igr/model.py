@@ -96,6 +96,20 @@ def batch_rep_pays(model, batch_size):
     return cache[batch_size]
 
 
+def load_checkpoint(path, device):
+    """torch.load that executes nothing from the file (weights_only), widened by
+    the three numpy names a pickled numpy integer scalar refers to - the keys of
+    the user_map / item_map dicts in a checkpoint IGCN.save of the reference
+    wrote (model.py:4208-4211: the maps are built from np.arange, 4147-4156)."""
+    import numpy.dtypes
+    try:
+        from numpy._core.multiarray import scalar
+    except ImportError:  # numpy < 2
+        from numpy.core.multiarray import scalar
+    with torch.serialization.safe_globals([scalar, np.dtype, numpy.dtypes.Int64DType]):
+        return torch.load(path, map_location=device, weights_only=True)
+
+
 class BasicModel(nn.Module):
     """model.py:35-53."""
 
@@ -108,6 +122,12 @@ class BasicModel(nn.Module):
         self.n_items = model_config['dataset'].n_items
         self.trainable = True
 
+    @property
+    def norm_vals(self):
+        """The adjacency's edge values by edge id (the reference keeps them inside
+        its sparse norm_adj; here they ride on the Graph generate_graph returns)."""
+        return self.norm_adj.values
+
     def predict(self, users):
         raise NotImplementedError
 
@@ -115,7 +135,7 @@ class BasicModel(nn.Module):
         torch.save(self.state_dict(), path)
 
     def load(self, path):
-        self.load_state_dict(torch.load(path, map_location=self.device, weights_only=True))
+        self.load_state_dict(load_checkpoint(path, self.device))
 
 
 class LightGCN(BasicModel):
@@ -126,14 +146,17 @@ class LightGCN(BasicModel):
         self.embedding_size = model_config['embedding_size']
         self.n_layers = model_config['n_layers']
         self.embedding = nn.Embedding(self.n_users + self.n_items, self.embedding_size)
-        self.norm_adj, self.norm_vals = self.generate_graph(model_config['dataset'])
+        self.norm_adj = self.generate_graph(model_config['dataset'])
         normal_(self.embedding.weight, std=0.1)
         self.to(device=self.device)
 
     def generate_graph(self, dataset):
+        """model.py:89-98: one object, as the reference's sparse norm_adj - the
+        Graph with its edge values attached (`.values`, what `norm_vals` reads)."""
         g, vals, self.degree, self.dinv = build_norm_adj(self.n_users, self.n_items, train_pairs(dataset),
                                                          self.device)
-        return g, vals
+        g.values = vals
+        return g
 
     def get_rep(self):
         """model.py:100-110, fused (one SpMM per layer, running layer mean)."""
@@ -189,7 +212,7 @@ class NGCF(BasicModel):
             [init_one_layer(self.layer_sizes[i - 1], self.layer_sizes[i]) for i in range(1, self.n_layers + 1)])
         self.bi_layers = nn.ModuleList(
             [init_one_layer(self.layer_sizes[i - 1], self.layer_sizes[i]) for i in range(1, self.n_layers + 1)])
-        self.norm_adj, self.norm_vals = self.generate_graph(model_config['dataset'])
+        self.norm_adj = self.generate_graph(model_config['dataset'])
         self.to(device=self.device)
 
     def generate_graph(self, dataset):
@@ -202,7 +225,9 @@ class NGCF(BasicModel):
         rp, ci, v, _ = csr_from_coo(row, col, n, n, None, dedup=True, want_eid=False)
         rs = row_sums(rp, v)
         vals = (v / np.repeat(rs, np.diff(rp))).astype(np.float32)
-        return Graph(rp, ci, n, n, device=self.device), torch.from_numpy(vals).to(self.device)
+        g = Graph(rp, ci, n, n, device=self.device)
+        g.values = torch.from_numpy(vals).to(self.device)
+        return g
 
     def dropout_values(self, vals):
         return dropout_values(self, vals)
@@ -263,7 +288,7 @@ class IGCN(BasicModel):
         self.n_layers = model_config['n_layers']
         self.dropout = model_config['dropout']
         self.feature_ratio = model_config['feature_ratio']
-        self.norm_adj, self.norm_vals = self.generate_graph(model_config['dataset'])
+        self.norm_adj = self.generate_graph(model_config['dataset'])
         self.alpha = 1.
         self.delta = model_config.get('delta', 0.99)
         self.feat_mat, self.user_map, self.item_map, self.row_sum = \
@@ -275,19 +300,30 @@ class IGCN(BasicModel):
         self.to(device=self.device)
 
     def generate_graph(self, dataset):
+        """model.py:89-98: one object, as the reference's sparse norm_adj - the
+        Graph with its edge values attached (`.values`, what `norm_vals` reads)."""
         g, vals, self.degree, self.dinv = build_norm_adj(self.n_users, self.n_items, train_pairs(dataset),
                                                          self.device)
-        return g, vals
+        g.values = vals
+        return g
 
     def update_feat_mat(self):
         """model.py:4127-4130: value = row_sum[row] ** ((alpha - 1)/2 - 0.5), on the device.
         The value is row-constant, so one value per row (feat_base) is kept; the
         per-edge array (feat_vals) is materialised only when asked for."""
         ex = (self.alpha - 1.) / 2. - 0.5
-        # in place once allocated: a captured training step (trainer.StepGraph) holds these pointers
-        self.feat_base = ops.feat_row_values(self.row_sum, ex, out=getattr(self, 'feat_base', None))
-        if getattr(self, '_feat_vals', None) is not None:
-            ops.feat_values(self.feat_mat, self.row_sum, ex, out=self._feat_vals)
+        # in place once allocated: a captured training step (trainer.StepGraph) holds these pointers.
+        # A feature graph regenerated for another dataset (generate_feat(..., is_updating=True) after
+        # new users / items arrived, model.py:4219) has other sizes: its buffers start afresh.
+        base = getattr(self, 'feat_base', None)
+        if base is not None and base.numel() != self.row_sum.numel():
+            base = None
+        fv = getattr(self, '_feat_vals', None)
+        if fv is not None and fv.numel() != self.feat_mat.nnz:
+            fv = self._feat_vals = None
+        self.feat_base = ops.feat_row_values(self.row_sum, ex, out=base)
+        if fv is not None:
+            ops.feat_values(self.feat_mat, self.row_sum, ex, out=fv)
 
     @property
     def feat_vals(self):
@@ -469,13 +505,14 @@ class IGCN(BasicModel):
                     'alpha': self.alpha}, path)
 
     def load(self, path):
-        """model.py:4213-4220.  Our own checkpoints hold only tensors, ints,
-        floats and dicts, so the restricted loader reads them."""
-        params = torch.load(path, map_location=self.device, weights_only=True)
+        """model.py:4213-4220.  Reads this class's checkpoints and the reference's
+        own (same keys; its user_map / item_map are keyed by numpy int64 scalars)
+        with the restricted loader: tensors, numbers and dicts only."""
+        params = load_checkpoint(path, self.device)
         self.load_state_dict(params['sate_dict'])
-        self.user_map = params['user_map']
-        self.item_map = params['item_map']
-        self.alpha = params['alpha']
+        self.user_map = {int(k): int(v) for k, v in params['user_map'].items()}
+        self.item_map = {int(k): int(v) for k, v in params['item_map'].items()}
+        self.alpha = float(params['alpha'])
         self.feat_mat, _, _, self.row_sum = self.generate_feat(self.config['dataset'], is_updating=True)
         self.update_feat_mat()
 
@@ -507,7 +544,7 @@ class AttIGCN(IGCN):
         self.feature_ratio = 1.
         self.alpha = 0.
         self.delta = model_config.get('delta', 0.99)
-        self.norm_adj, self.norm_vals = self.generate_graph(model_config['dataset'])
+        self.norm_adj = self.generate_graph(model_config['dataset'])
         self.feat_mat, self.user_map, self.item_map, self.row_sum = self.generate_feat(model_config['dataset'])
         self.update_feat_mat()
         self.embedding = nn.Embedding(self.feat_mat.n_cols, self.embedding_size)

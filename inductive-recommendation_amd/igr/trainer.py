@@ -111,6 +111,9 @@ class BasicTrainer:
         self.save_path = None
         self.opt = None
         self.verbose = trainer_config.get('verbose', True)
+        # True while train() runs (or when the caller vouches that train / val / test lists stay
+        # as they are): eval() then reuses the exclusion CSR and the metric keys between calls
+        self.static_eval_lists = trainer_config.get('static_eval_lists', False)
 
     def initialize_optimizer(self):
         opt = getattr(sys.modules[__name__], self.config['optimizer'])
@@ -122,16 +125,31 @@ class BasicTrainer:
     def train(self, verbose=True, writer=None):
         """trainer.py:58-113."""
         if not self.model.trainable:
-            _, metrics = self.eval('val')
+            _, metrics, _ = self.eval('val')
             return metrics['NDCG'][self.topks[5]]
         ckpt_dir = self.config.get('checkpoint_dir', 'checkpoints')
         os.makedirs(ckpt_dir, exist_ok=True)
+        static, self.static_eval_lists = self.static_eval_lists, True  # nothing edits the lists in here
+        try:
+            self._epochs(verbose, writer, ckpt_dir)
+        finally:
+            self.static_eval_lists = static
+            if not static:
+                self.__dict__.pop('_excl', None)
+                self.__dict__.pop('_eval_keys', None)
+        self._close_step_graph()  # load() below rebuilds graph structures a captured step points at
+        if self.save_path:
+            self.model.load(self.save_path)
+        return self.best_ndcg
+
+    def _epochs(self, verbose, writer, ckpt_dir):
+        """The epoch loop of train(): trainer.py:69-110."""
         patience = self.max_patience
         for self.epoch in range(self.n_epochs):
             start = time.time()
             self.model.train()
             loss = self.train_one_epoch()
-            _, metrics = self.eval('train')
+            _, metrics, _ = self.eval('train')
             if verbose:
                 print('Epoch {:d}/{:d}, Loss: {:.6f}, Time: {:.3f}s'.format(self.epoch, self.n_epochs, loss,
                                                                           time.time() - start))
@@ -140,7 +158,7 @@ class BasicTrainer:
             if (self.epoch + 1) % self.val_interval != 0:
                 continue
             start = time.time()
-            results, metrics = self.eval('val')
+            results, metrics, _ = self.eval('val')
             if verbose:
                 print('Validation result. {:s}Time: {:.3f}s'.format(results, time.time() - start))
             ndcg = metrics['NDCG'][self.topks[4]]
@@ -160,10 +178,6 @@ class BasicTrainer:
                     if verbose:
                         print('Early stopping!')
                     break
-        self._close_step_graph()  # load() below rebuilds graph structures a captured step points at
-        if self.save_path:
-            self.model.load(self.save_path)
-        return self.best_ndcg
 
     def _close_step_graph(self):
         sg = getattr(self, '_step_graph', None)
@@ -180,13 +194,17 @@ class BasicTrainer:
         return None
 
     def calculate_metrics(self, eval_data, rec_items):
-        # the eval lists never change during training: their keys are built once
-        cache = self.__dict__.setdefault('_eval_keys', {})
         n_items = max(int(self.dataset.n_items), int(rec_items.max(initial=0)) + 1)
+        if not self.static_eval_lists:
+            return calculate_metrics(eval_data, rec_items, self.topks,
+                                     keys=eval_keys(eval_data, rec_items.shape[0], n_items) + (n_items,))
+        # inside train() the eval lists do not change: their keys are built once (the entry
+        # holds the list object, so its id cannot pass to another list)
+        cache = self.__dict__.setdefault('_eval_keys', {})
         key = (id(eval_data), len(eval_data), rec_items.shape[0], n_items)
         if key not in cache:
-            cache[key] = eval_keys(eval_data, rec_items.shape[0], n_items) + (n_items,)
-        return calculate_metrics(eval_data, rec_items, self.topks, keys=cache[key])
+            cache[key] = (eval_data, eval_keys(eval_data, rec_items.shape[0], n_items) + (n_items,))
+        return calculate_metrics(eval_data, rec_items, self.topks, keys=cache[key][1])
 
     @torch.no_grad()
     def rank(self, val_or_test, banned_items=None):
@@ -200,8 +218,9 @@ class BasicTrainer:
         rep = self.model.get_rep()
         excl = None
         if val_or_test != 'train':
-            # the exclusion lists never change during training: one device CSR per split
-            cache = self.__dict__.setdefault('_excl', {})
+            # inside train() the exclusion lists do not change: one device CSR per split,
+            # otherwise rebuilt from the lists at every call, as the reference reads them
+            cache = self.__dict__.setdefault('_excl', {}) if self.static_eval_lists else {}
             ck = (val_or_test, id(self.dataset.train_data), id(self.dataset.val_data), n_users)
             if ck not in cache:
                 lists = self.dataset.train_data
@@ -209,7 +228,8 @@ class BasicTrainer:
                     lists = [a + b for a, b in zip(self.dataset.train_data, self.dataset.val_data)]
                 ptr, flat = _csr(lists, n_users)
                 cache[ck] = (torch.from_numpy(ptr.astype(np.int64)).to(self.device),
-                             torch.from_numpy(flat.astype(np.int32)).to(self.device))
+                             torch.from_numpy(flat.astype(np.int32)).to(self.device),
+                             self.dataset.train_data, self.dataset.val_data)
             excl = cache[ck]
         kmax = max(self.topks)
         rec = []
@@ -231,7 +251,8 @@ class BasicTrainer:
         return torch.cat(rec).cpu().numpy()
 
     def eval(self, val_or_test, banned_items=None):
-        """trainer.py:146-210; returns (result string, metrics).
+        """trainer.py:146-210; returns the reference's triple (result string,
+        metrics, prot_results), the last one the empty list it is there (184-210).
 
         The reference iterates its test_user_loader (a torch DataLoader,
         trainer.py:41-42, 151), and creating a DataLoader iterator draws one
@@ -244,7 +265,39 @@ class BasicTrainer:
         metrics = self.calculate_metrics(eval_data, rec_items)
         fmt = lambda m: ''.join('{:.3f}, '.format(metrics[m][k] * 100.) for k in self.topks)  # noqa: E731
         results = 'Precision: {:s}Recall: {:s}NDCG: {:s}'.format(fmt('Precision'), fmt('Recall'), fmt('NDCG'))
-        return results, metrics
+        return results, metrics, []
+
+    def inductive_eval(self, n_old_users, n_old_items):
+        """trainer.py:212-253: the test metrics of a model moved to a grown dataset,
+        over six slices - all / old / new users on all items, all users on old /
+        new items (the other items banned from the ranking), old users on old
+        items.  Prints the reference's six lines; also returns the metrics by
+        slice (the reference returns nothing).  dataset.test_data is left as found."""
+        ds = self.dataset
+        full = ds.test_data
+        n_users, n_items = ds.n_users, ds.n_items
+        old_items = lambda u: [i for i in full[u] if i < n_old_items]  # noqa: E731
+        new_items = lambda u: [i for i in full[u] if i >= n_old_items]  # noqa: E731
+        ban_new = np.arange(n_old_items, n_items)
+        ban_old = np.arange(n_old_items)
+        slices = [
+            ('All users and all items', lambda u: full[u], None),
+            ('Old users and all items', lambda u: full[u] if u < n_old_users else [], None),
+            ('New users and all items', lambda u: full[u] if u >= n_old_users else [], None),
+            ('All users and old items', old_items, ban_new),
+            ('All users and new items', new_items, ban_old),
+            ('Old users and old items', lambda u: old_items(u) if u < n_old_users else [], ban_new),
+        ]
+        out = {}
+        try:
+            for name, pick, banned in slices:
+                ds.test_data = [list(pick(u)) for u in range(n_users)]
+                results, metrics, _ = self.eval('test', banned_items=banned)
+                print('{:s} result. {:s}'.format(name, results))
+                out[name] = metrics
+        finally:
+            ds.test_data = full
+        return out
 
 
 class StepGraph:

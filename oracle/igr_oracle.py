@@ -136,16 +136,29 @@ def norm_adj(n_users, n_items, train_array):
     return A
 
 
-def generate_feat(n_users, n_items, train_array):
-    """IGCN.generate_feat with feature_ratio = 1 (model.py:4139-4175).
-    user u -> column U + i for each training item; item i -> column u;
-    every user -> column U + I; every item -> column U + I + 1.  row_sum = row degree."""
+def generate_feat(n_users, n_items, train_array, user_map=None, item_map=None):
+    """IGCN.generate_feat (model.py:4139-4175).
+    user u -> column U' + item_map[i] for each training item i in item_map; item i ->
+    column user_map[u] for each training user u in user_map; every user -> column
+    U' + I'; every item -> column U' + I' + 1 (U', I' = the sizes of the maps).
+    Maps None: feature_ratio = 1 on this dataset (identity maps, 4147-4156); maps
+    given: is_updating=True (4157-4159) - the maps of the dataset the model was
+    built on, applied to a dataset that has grown since.  row_sum = row degree."""
     ta = np.asarray(train_array, dtype=np.int64).reshape(-1, 2)
     u, i = ta[:, 0], ta[:, 1]
     U, I = n_users, n_items
-    row = np.concatenate([u, U + i, np.arange(U), U + np.arange(I)])
-    col = np.concatenate([U + i, u, np.full(U, U + I), np.full(I, U + I + 1)])
-    F = coo_to_csr(U + I, U + I + 2, row, col, None, dedup=True)
+    umap = np.arange(U, dtype=np.int64) if user_map is None else np.full(U, -1, np.int64)
+    imap = np.arange(I, dtype=np.int64) if item_map is None else np.full(I, -1, np.int64)
+    for m, table in ((user_map, umap), (item_map, imap)):
+        if m is not None:
+            for k, v in m.items():
+                table[int(k)] = int(v)
+    Ud = U if user_map is None else len(user_map)
+    Id = I if item_map is None else len(item_map)
+    ki, ku = imap[i] >= 0, umap[u] >= 0
+    row = np.concatenate([u[ki], U + i[ku], np.arange(U), U + np.arange(I)])
+    col = np.concatenate([Ud + imap[i[ki]], umap[u[ku]], np.full(U, Ud + Id), np.full(I, Ud + Id + 1)])
+    F = coo_to_csr(U + I, Ud + Id + 2, row, col, None, dedup=True)
     F.row_sum = row_sums(F)
     return F
 
@@ -300,14 +313,38 @@ def calculate_metrics(eval_data, rec_items, topks):
     return res
 
 
-def eval_metrics(rep, n_users, train_data, eval_data, split, topks):
+def eval_metrics(rep, n_users, train_data, eval_data, split, topks, banned_items=None):
     """BasicTrainer.eval (trainer.py:146-170) with LightGCN.predict (model.py:122-127):
     scores = rep[u] . rep[items]^T; train items (and val items for 'test') set to -inf
-    except for split 'train'; top-max(topks); then calculate_metrics."""
+    except for split 'train'; banned items set to -inf for every user (166-167);
+    top-max(topks); then calculate_metrics."""
     scores = rep[:n_users] @ rep[n_users:].T
     if split != 'train':
         for u in range(n_users):
             scores[u, train_data[u]] = -np.inf
+    if banned_items is not None:
+        scores[:, banned_items] = -np.inf
     kmax = max(topks)
     rec = np.argsort(-scores, axis=1, kind='stable')[:, :kmax]
     return calculate_metrics(eval_data, rec, topks)
+
+
+INDUCTIVE_SLICES = ['All users and all items', 'Old users and all items', 'New users and all items',
+                    'All users and old items', 'All users and new items', 'Old users and old items']
+
+
+def inductive_eval(rep, n_users, n_items, exclude, test_data, n_old_users, n_old_items, topks):
+    """BasicTrainer.inductive_eval (trainer.py:212-253): the 'test' metrics over six
+    slices of the test lists, in the order of INDUCTIVE_SLICES.  `exclude` = train + val
+    lists (what eval('test') masks)."""
+    olds = [[i for i in x if i < n_old_items] for x in test_data]
+    news = [[i for i in x if i >= n_old_items] for x in test_data]
+    cut = lambda lists, keep: [x if keep(u) else [] for u, x in enumerate(lists)]  # noqa: E731
+    ban_new, ban_old = np.arange(n_old_items, n_items), np.arange(n_old_items)
+    cases = [(test_data, None),
+             (cut(test_data, lambda u: u < n_old_users), None),
+             (cut(test_data, lambda u: u >= n_old_users), None),
+             (olds, ban_new), (news, ban_old),
+             (cut(olds, lambda u: u < n_old_users), ban_new)]
+    return {name: eval_metrics(rep, n_users, exclude, data, 'test', topks, banned)
+            for name, (data, banned) in zip(INDUCTIVE_SLICES, cases)}

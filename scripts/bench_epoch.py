@@ -45,7 +45,8 @@ def main():
                     'feature_ratio': 1., 'dataset': DS()})
         tr = T.get_trainer({'name': 'IGCNTrainer', 'optimizer': 'Adam', 'lr': 1e-3, 'l2_reg': 0., 'aux_reg': 0.01,
                             'device': dev, 'n_epochs': args.epochs, 'batch_size': 2048, 'test_batch_size': 512,
-                            'topks': [1, 5, 10, 15, 20], 'graph': graph, 'seed': 1}, DS(), m)
+                            'topks': [1, 5, 10, 15, 20], 'graph': graph, 'seed': 1,
+                            'static_eval_lists': True}, DS(), m)  # as inside train(): the lists stay put
         ep_s, recall, parts = [], [], []
         for _ in range(args.epochs):
             torch.cuda.synchronize()
@@ -54,9 +55,9 @@ def main():
             tr.train_one_epoch()
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            _, vm = tr.eval('val')
+            _, vm, _ = tr.eval('val')
             t2 = time.perf_counter()
-            _, tm = tr.eval('test')
+            _, tm, _ = tr.eval('test')
             torch.cuda.synchronize()
             t3 = time.perf_counter()
             ep_s.append(t3 - t0)

@@ -86,8 +86,8 @@ def test_igcn_training_matches_reference(shape, batch_rep):
             if ep == 0 and s < 20:
                 first.append(loss)
         m.feat_mat_anneal()
-        _, vmet = tr.eval('val')
-        _, tmet = tr.eval('test')
+        _, vmet, _ = tr.eval('val')
+        _, tmet, _ = tr.eval('test')
         log['loss'].append(tot / spe)
         log['val_recall20'].append(float(vmet['Recall'][20]))
         log['test_recall20'].append(float(tmet['Recall'][20]))
@@ -142,8 +142,8 @@ def test_lightgcn_bpr_training_matches_reference(shape, batch_rep):
             tot += loss
             if ep == 0 and s < 20:
                 first.append(loss)
-        _, vmet = tr.eval('val')
-        _, tmet = tr.eval('test')
+        _, vmet, _ = tr.eval('val')
+        _, tmet, _ = tr.eval('test')
         log['loss'].append(tot / spe)
         log['val_recall20'].append(float(vmet['Recall'][20]))
         log['test_recall20'].append(float(tmet['Recall'][20]))

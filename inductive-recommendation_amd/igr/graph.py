@@ -10,6 +10,7 @@ Layout in HBM:
     order    int32[n_order]    rows of degree <= split_threshold, heaviest first
     split_row int32, split_ptr int64, chunk_row int32, chunk_beg int64  (long rows)
 """
+import copy
 import ctypes
 
 import numpy as np
@@ -165,8 +166,22 @@ class Graph:
             v = vv
         return g, v
 
+    values = None  # float32[nnz] by edge id when the graph carries its edge values (model.norm_adj)
+
+    def with_values(self, values):
+        """This graph with another set of edge values - what the reference holds as a
+        second sparse tensor over the same indices (NGCF.dropout_sp_mat, model.py:4016-4028).
+        A view: device arrays, schedule, workspaces and the reverse graph stay the base graph's."""
+        g = copy.copy(self)
+        g._base = getattr(self, '_base', None) or self
+        g.values = values
+        return g
+
     def reverse(self):
         """Reverse graph for gspmm backward; its edge ids are this graph's edge ids."""
+        base = getattr(self, '_base', None)
+        if base is not None:
+            return base.reverse()
         if self._reverse is None:
             h = self._host
             t_rp, t_ci, t_pos = csr_transpose(h['row_ptr'], h['col_idx'], self.n_rows, self.n_cols)

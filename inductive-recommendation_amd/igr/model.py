@@ -232,6 +232,14 @@ class NGCF(BasicModel):
     def dropout_values(self, vals):
         return dropout_values(self, vals)
 
+    def dropout_sp_mat(self, mat):
+        """model.py:4016-4028, same call: `mat` a graph carrying edge values (norm_adj,
+        or the feat_mat of an IGCN passed as self, as at model.py:4189); returns that
+        graph with the dropped values (a view, Graph.with_values).  The fused paths
+        (get_rep) draw the same masks without materialising this."""
+        counter = mat if hasattr(self, 'next_dropout_step') else None  # IGCN: the fused path's draws
+        return mat.with_values(dropout_values(self, graph_values(self, mat), counter))
+
     def get_rep(self):
         representations = self.embedding.weight
         all_layer_rep = [representations]
@@ -256,6 +264,16 @@ class NGCF(BasicModel):
 
     def predict(self, users, rep=None):
         return LightGCN.predict(self, users, rep)
+
+
+def graph_values(model, mat):
+    """The edge values of `mat` by edge id: the ones it carries, or the model's
+    feature values when it is the model's feature graph."""
+    if mat.values is not None:
+        return mat.values
+    if mat is getattr(model, 'feat_mat', None):
+        return model.feat_vals
+    raise ValueError('this graph carries no edge values')
 
 
 def dropout_values(model, vals, graph=None):
@@ -402,7 +420,11 @@ class IGCN(BasicModel):
         return self._drop_seed, self._drop_step, None
 
     def inductive_rep_layer(self, feat_vals):
-        """model.py:4177-4186 (no padding needed: the lhs has n_cols rows)."""
+        """model.py:4177-4186 (no padding needed: the lhs has n_cols rows).  Takes the
+        reference's argument - the feature graph with its (dropped) values - or the
+        values alone."""
+        if isinstance(feat_vals, Graph):
+            feat_vals = graph_values(self, feat_vals)
         if isinstance(feat_vals, ops.ScaledWeights):
             return ops.propagate(self.norm_adj, self.embedding.weight, 0, feat=self.feat_mat, fvals=feat_vals)
         return ops.gspmm(self.feat_mat, 'mul', 'sum', self.embedding.weight, feat_vals)
@@ -596,6 +618,8 @@ class AttIGCN(IGCN):
         return d in (32, 64, 128, 256) and H in (1, 2, 4, 8) and H * d <= 512
 
     def inductive_rep_layer(self, feat_vals, return_alpha=False):
+        if isinstance(feat_vals, Graph):
+            feat_vals = graph_values(self, feat_vals)
         w = self.attention_values(feat_vals)
         if return_alpha:
             return w

@@ -122,6 +122,13 @@ class BasicTrainer:
     def train_one_epoch(self):
         raise NotImplementedError
 
+    def record(self, writer, stage, metrics):
+        """trainer.py:49-56: every metric@k of one eval to a tensorboard-style writer."""
+        for metric in metrics:
+            for k in self.topks:
+                writer.add_scalar('{:s}_{:s}/{:s}_{:s}@{:d}'.format(self.model.name, self.name, stage, metric, k),
+                                  metrics[metric][k], self.epoch)
+
     def train(self, verbose=True, writer=None):
         """trainer.py:58-113."""
         if not self.model.trainable:
@@ -155,12 +162,15 @@ class BasicTrainer:
                                                                           time.time() - start))
             if writer:
                 writer.add_scalar('{:s}_{:s}/train_loss'.format(self.model.name, self.name), loss, self.epoch)
+                self.record(writer, 'train', metrics)
             if (self.epoch + 1) % self.val_interval != 0:
                 continue
             start = time.time()
             results, metrics, _ = self.eval('val')
             if verbose:
                 print('Validation result. {:s}Time: {:.3f}s'.format(results, time.time() - start))
+            if writer:
+                self.record(writer, 'validation', metrics)
             ndcg = metrics['NDCG'][self.topks[4]]
             if ndcg > self.best_ndcg:
                 if self.save_path and os.path.exists(self.save_path):

@@ -1,6 +1,8 @@
-"""igr.utils - run set-up helpers with the names the reference's scripts call
-(`set_seed`, `init_run`; /root/reference utils.py:13-30).  The epoch loss is
-accumulated on the device by the trainers, so no host-side meter is needed."""
+"""igr.utils - the helpers of the reference's utils.py that its scripts and models
+call by name: run set-up (`set_seed`, `init_run`, utils.py:13-30) and graph
+construction (`generate_daj_mat`, `get_sparse_tensor`, `graph_rank_nodes`,
+utils.py:33-50, 186-215).  The epoch loss is accumulated on the device by the
+trainers, so no host-side meter is needed."""
 import os
 import random
 import sys
@@ -27,3 +29,38 @@ def init_run(log_path, seed):
     log = open(os.path.join(log_path, 'lo00gg.txt'), 'w', buffering=1)
     sys.stdout = sys.stderr = log
     return log
+
+
+def generate_daj_mat(dataset):
+    """utils.py:42-50: the symmetric bipartite adjacency [[0, R], [R^T, 0]] of the
+    training pairs as a scipy CSR matrix, duplicates summed - built by the
+    library's C++ CSR builder (igr_csr_from_coo), not by scipy's."""
+    import scipy.sparse as sp
+    from .graph import csr_from_coo
+    from .model import train_pairs
+    pairs = train_pairs(dataset)
+    U, n = dataset.n_users, dataset.n_users + dataset.n_items
+    row = np.concatenate([pairs[:, 0], pairs[:, 1] + U])
+    col = np.concatenate([pairs[:, 1] + U, pairs[:, 0]])
+    rp, ci, v, _ = csr_from_coo(row, col, n, n, None, dedup=True, want_eid=False)
+    return sp.csr_matrix((v, ci, rp), shape=(n, n), dtype=np.float32)
+
+
+def get_sparse_tensor(mat, device):
+    """utils.py:33-39: a scipy sparse matrix as the device object the models
+    propagate over - here a Graph (CSR + schedule in HBM) carrying the float32
+    values by edge id (`.values`), edge id = position in (row, col) order, the
+    order of the reference's coalesced COO tensor."""
+    from .graph import Graph, csr_from_coo
+    coo = mat.tocoo()
+    rp, ci, v, _ = csr_from_coo(coo.row, coo.col, mat.shape[0], mat.shape[1], coo.data.astype(np.float32),
+                                dedup=True, want_eid=False)
+    g = Graph(rp, ci, mat.shape[0], mat.shape[1], device=device)
+    g.values = torch.from_numpy(v).to(device)
+    return g
+
+
+def graph_rank_nodes(dataset, ranking_metric):
+    """utils.py:186-215 ('degree', 'sort' / 'greedy')."""
+    from .model import graph_rank_nodes as rank
+    return rank(dataset, ranking_metric)

@@ -190,3 +190,43 @@ def test_batch_edges_estimate_by_hand():
     rp = np.searchsorted(row, np.arange(6)).astype(np.int64)
     est = M.batch_edges_estimate(rp, col.astype(np.int32), 2, 10)
     assert est == pytest.approx(10 * (1.5 + 1.75 + 1.0))
+
+
+def test_utils_graph_helpers_by_the_reference_names(golden):
+    """utils.generate_daj_mat (utils.py:42-50) bit-exact; utils.get_sparse_tensor (33-39) of the
+    matrix LightGCN.generate_graph forms (model.py:89-98) carries the reference's values in
+    its coalesced order."""
+    import scipy.sparse as sp
+    from igr import utils
+
+    class DS:
+        n_users, n_items = int(golden['n_users']), int(golden['n_items'])
+        train_array = golden['train_array'].tolist()
+    adj = utils.generate_daj_mat(DS())
+    assert adj.dtype == np.float32 and adj.shape == (DS.n_users + DS.n_items,) * 2
+    np.testing.assert_array_equal(adj.indptr, golden['adj_indptr'])
+    np.testing.assert_array_equal(adj.indices, golden['adj_indices'])
+    np.testing.assert_array_equal(adj.data, golden['adj_data'])
+    degree = np.array(np.sum(adj, axis=1)).squeeze()
+    degree = np.maximum(1., degree)
+    d = sp.diags(np.power(degree, -0.5), format='csr', dtype=np.float32)
+    g = utils.get_sparse_tensor(d.dot(adj).dot(d), 'cpu')
+    h = g.host()
+    np.testing.assert_array_equal(np.repeat(np.arange(g.n_rows), np.diff(h['row_ptr'])), golden['norm_idx'][0])
+    np.testing.assert_array_equal(h['col_idx'], golden['norm_idx'][1])
+    np.testing.assert_array_equal(g.values.numpy(), golden['norm_val'])
+    # a second set of values over the same graph is a view: one reverse graph, base untouched
+    v2 = g.values * 2
+    g2 = g.with_values(v2)
+    assert g2.values is v2 and g.values is not v2 and g2.reverse() is g.reverse() and g2.csr is g.csr
+
+
+def test_trainer_record_writes_every_metric_at_every_k():
+    """BasicTrainer.record (trainer.py:49-56)."""
+    import types
+    seen = []
+    writer = types.SimpleNamespace(add_scalar=lambda tag, v, step: seen.append((tag, v, step)))
+    me = types.SimpleNamespace(topks=[1, 5], model=types.SimpleNamespace(name='IGCN'), name='IGCNTrainer', epoch=3)
+    T.BasicTrainer.record(me, writer, 'validation', {'Recall': {1: .1, 5: .5}, 'NDCG': {1: .2, 5: .6}})
+    assert seen == [('IGCN_IGCNTrainer/validation_Recall@1', .1, 3), ('IGCN_IGCNTrainer/validation_Recall@5', .5, 3),
+                    ('IGCN_IGCNTrainer/validation_NDCG@1', .2, 3), ('IGCN_IGCNTrainer/validation_NDCG@5', .6, 3)]

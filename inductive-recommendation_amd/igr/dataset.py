@@ -252,8 +252,11 @@ class ProcessedDataset(BasicDataset):
 
 
 class AuxiliaryDataset(BasicDataset):
-    """dataset.py:258-273: training data restricted to / renumbered by the
-    template-feature maps of an inductive model."""
+    """dataset.py:258-273: the training data restricted to, and renumbered by, the
+    template-feature maps of an inductive model (user u -> user_map[u], item i ->
+    item_map[i]; pairs with an unmapped end are left out).  Vectorised over the
+    pair array; the per-user lists (same order as the dataset's) are built only if
+    a host-side sampler asks for them."""
 
     def __init__(self, dataset, user_map, item_map):
         self.name = 'AuxiliaryDataset'
@@ -262,17 +265,42 @@ class AuxiliaryDataset(BasicDataset):
         self.device = getattr(dataset, 'device', 'cpu')
         self.negative_sample_ratio = 1
         self.length = len(dataset)
-        self._pairs = None
-        self.train_data = [[] for _ in range(self.n_users)]
-        for o_user in range(dataset.n_users):
-            if o_user in user_map:
-                for o_item in dataset.train_data[o_user]:
-                    if o_item in item_map:
-                        self.train_data[user_map[o_user]].append(item_map[o_item])
-        self.train_array = [[u, i] for u in range(self.n_users) for i in self.train_data[u]]
+        pairs = dataset.train_pairs if hasattr(dataset, 'train_pairs') else \
+            np.asarray(dataset.train_array, dtype=np.int64).reshape(-1, 2)
+        u = _map_array(user_map, dataset.n_users)[pairs[:, 0]]
+        i = _map_array(item_map, dataset.n_items)[pairs[:, 1]]
+        keep = (u >= 0) & (i >= 0)
+        u, i = u[keep], i[keep]
+        # train_array lists each user's items in train_data order (dataset.py:155-160), so a
+        # stable sort by the new user id gives the reference's lists
+        order = np.argsort(u, kind='stable')
+        self._pairs = np.stack([u[order], i[order]], axis=1)
+        self.train_array = self._pairs
+        self._train_data = None
+        self.val_data = self.test_data = None
+
+    @property
+    def train_data(self):
+        if self._train_data is None:
+            ptr = np.searchsorted(self._pairs[:, 0], np.arange(self.n_users + 1))
+            items = self._pairs[:, 1]
+            self._train_data = [items[ptr[k]:ptr[k + 1]].tolist() for k in range(self.n_users)]
+        return self._train_data
+
+    @train_data.setter
+    def train_data(self, v):
+        self._train_data = v
 
     def __len__(self):
         return self.length
+
+
+def _map_array(id_map, n):
+    """A {old id: new id} dict as an int64 lookup array over [0, n), -1 where unmapped."""
+    a = np.full(n, -1, np.int64)
+    if id_map:
+        a[np.fromiter(id_map.keys(), np.int64, len(id_map))] = np.fromiter(id_map.values(), np.int64, len(id_map))
+    return a
 
 
 class SyntheticDataset(BasicDataset):

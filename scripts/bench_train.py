@@ -79,8 +79,6 @@ def main():
     m = getattr(M, args.model)({'name': args.model, 'embedding_size': args.d, 'n_layers': args.layers,
                                 'device': dev, 'dropout': 0.3, 'feature_ratio': 1., 'dataset': ds,
                                 'batch_rep': {'auto': 'auto', 'true': True, 'false': False}[args.batch_rep]})
-    # AuxiliaryDataset needs per-user lists; with feature_ratio = 1 it is the dataset itself
-    T.AuxiliaryDataset = lambda dataset, um, im: dataset
     igcn = args.model != 'LightGCN'
     tr = T.get_trainer({'name': 'IGCNTrainer' if igcn else 'BPRTrainer', 'optimizer': 'Adam', 'lr': 1e-3,
                         'l2_reg': 0., 'aux_reg': 0.01, 'device': dev, 'n_epochs': 1, 'batch_size': args.batch,

@@ -71,7 +71,7 @@ def _single(pairs, emb0, batch_lists):
         opt.zero_grad()
         tot.backward()
         opt.step()
-        losses.append(float(tot))
+        losses.append(float(tot.detach()))
     return losses, m.embedding.weight.detach().cpu().numpy(), m.w.detach().cpu().numpy()
 
 

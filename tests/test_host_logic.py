@@ -230,3 +230,34 @@ def test_trainer_record_writes_every_metric_at_every_k():
     T.BasicTrainer.record(me, writer, 'validation', {'Recall': {1: .1, 5: .5}, 'NDCG': {1: .2, 5: .6}})
     assert seen == [('IGCN_IGCNTrainer/validation_Recall@1', .1, 3), ('IGCN_IGCNTrainer/validation_Recall@5', .5, 3),
                     ('IGCN_IGCNTrainer/validation_NDCG@1', .2, 3), ('IGCN_IGCNTrainer/validation_NDCG@5', .6, 3)]
+
+
+def test_auxiliary_dataset_restricts_and_renumbers():
+    """AuxiliaryDataset (dataset.py:258-273) against its definition, with maps that
+    cover part of the users / items in shuffled order (feature_ratio < 1)."""
+    rng = np.random.RandomState(4)
+    nu, ni = 40, 30
+
+    lists = [rng.permutation(ni)[:rng.randint(0, 9)].tolist() for _ in range(nu)]
+
+    class DS:
+        n_users, n_items, device = nu, ni, 'cpu'
+        train_data = lists
+        train_array = [[u, i] for u in range(nu) for i in lists[u]]
+
+        def __len__(self):
+            return len(self.train_array)
+    user_map = {int(u): k for k, u in enumerate(rng.permutation(nu)[:25])}
+    item_map = {int(i): k for k, i in enumerate(rng.permutation(ni)[:18])}
+    aux = D.AuxiliaryDataset(DS(), user_map, item_map)
+    want = [[] for _ in range(len(user_map))]
+    for o_user in range(nu):
+        if o_user in user_map:
+            want[user_map[o_user]] += [item_map[i] for i in DS.train_data[o_user] if i in item_map]
+    assert (aux.n_users, aux.n_items, len(aux)) == (25, 18, len(DS.train_array))
+    assert aux.train_data == want
+    assert aux.train_pairs.tolist() == [[u, i] for u in range(25) for i in want[u]]
+    ident = D.AuxiliaryDataset(DS(), {u: u for u in range(nu)}, {i: i for i in range(ni)})
+    assert ident.train_data == DS.train_data
+    empty = D.AuxiliaryDataset(DS(), {}, {})
+    assert (empty.n_users, empty.n_items, empty.train_data, len(empty.train_pairs)) == (0, 0, [], 0)

@@ -270,11 +270,7 @@ class AuxiliaryDataset(BasicDataset):
         u = _map_array(user_map, dataset.n_users)[pairs[:, 0]]
         i = _map_array(item_map, dataset.n_items)[pairs[:, 1]]
         keep = (u >= 0) & (i >= 0)
-        u, i = u[keep], i[keep]
-        # train_array lists each user's items in train_data order (dataset.py:155-160), so a
-        # stable sort by the new user id gives the reference's lists
-        order = np.argsort(u, kind='stable')
-        self._pairs = np.stack([u[order], i[order]], axis=1)
+        self._pairs = np.stack([u[keep], i[keep]], axis=1)  # in the dataset's pair order
         self.train_array = self._pairs
         self._train_data = None
         self.val_data = self.test_data = None
@@ -282,8 +278,11 @@ class AuxiliaryDataset(BasicDataset):
     @property
     def train_data(self):
         if self._train_data is None:
-            ptr = np.searchsorted(self._pairs[:, 0], np.arange(self.n_users + 1))
-            items = self._pairs[:, 1]
+            # train_array lists each user's items in train_data order (dataset.py:155-160), so a
+            # stable sort by the new user id gives the reference's lists
+            order = np.argsort(self._pairs[:, 0], kind='stable')
+            ptr = np.searchsorted(self._pairs[order, 0], np.arange(self.n_users + 1))
+            items = self._pairs[order, 1]
             self._train_data = [items[ptr[k]:ptr[k + 1]].tolist() for k in range(self.n_users)]
         return self._train_data
 

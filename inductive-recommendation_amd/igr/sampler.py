@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from .graph import csr_from_coo
 
 
 class DeviceBPRSampler:
@@ -21,18 +22,16 @@ class DeviceBPRSampler:
         pairs = dataset.train_pairs if hasattr(dataset, 'train_pairs') else \
             np.asarray(dataset.train_array, np.int64).reshape(-1, 2)
         self.n_users, self.n_items = dataset.n_users, dataset.n_items
-        order = np.lexsort((pairs[:, 1], pairs[:, 0]))
-        p = pairs[order]
-        keep = np.ones(len(p), bool)
-        keep[1:] = (p[1:, 0] != p[:-1, 0]) | (p[1:, 1] != p[:-1, 1])  # membership lists are sets
-        p = p[keep]
-        row_ptr = np.searchsorted(p[:, 0], np.arange(self.n_users + 1)).astype(np.int64)
+        # membership lists are sets: each user's distinct items, ascending - the duplicate-merging
+        # CSR of the pairs (the multithreaded C++ builder; a numpy lexsort takes 20x as long)
+        row_ptr, items, _, _ = csr_from_coo(pairs[:, 0], pairs[:, 1], self.n_users, self.n_items, None,
+                                            dedup=True, want_eid=False)
         active = np.nonzero(np.diff(row_ptr) > 0)[0].astype(np.int32)
         if len(active) == 0:
             raise ValueError('no user has training items')
         self.device = torch.device(device)
         self.row_ptr = torch.from_numpy(row_ptr).to(self.device)
-        self.items = torch.from_numpy(p[:, 1].astype(np.int32)).to(self.device)
+        self.items = torch.from_numpy(np.ascontiguousarray(items, dtype=np.int32)).to(self.device)
         self.active = torch.from_numpy(active).to(self.device)
         self.batch_size, self.seed, self.max_rounds = batch_size, int(seed), max_rounds
         self.length = len(dataset)

@@ -283,7 +283,7 @@ class AuxiliaryDataset(BasicDataset):
             order = np.argsort(self._pairs[:, 0], kind='stable')
             ptr = np.searchsorted(self._pairs[order, 0], np.arange(self.n_users + 1))
             items = self._pairs[order, 1]
-            self._train_data = [items[ptr[k]:ptr[k + 1]].tolist() for k in range(self.n_users)]
+            self._train_data = _lists(items, ptr)
         return self._train_data
 
     @train_data.setter
@@ -292,6 +292,12 @@ class AuxiliaryDataset(BasicDataset):
 
     def __len__(self):
         return self.length
+
+
+def _lists(items, ptr):
+    """CSR (items, row_ptr) as a list of per-row Python lists (one tolist, then slices)."""
+    flat, p = items.tolist(), ptr.tolist()
+    return [flat[a:b] for a, b in zip(p[:-1], p[1:])]
 
 
 def _map_array(id_map, n):
@@ -327,7 +333,7 @@ class SyntheticDataset(BasicDataset):
             order = np.argsort(self._pairs[:, 0], kind='stable')
             items = self._pairs[order, 1]
             ptr = np.searchsorted(self._pairs[order, 0], np.arange(self.n_users + 1))
-            self._train_data = [items[ptr[u]:ptr[u + 1]].tolist() for u in range(self.n_users)]
+            self._train_data = _lists(items, ptr)
         return self._train_data
 
     @train_data.setter

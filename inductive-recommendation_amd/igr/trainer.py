@@ -17,6 +17,7 @@ step (StepGraph) instead of issuing every launch from Python.  The epoch loss is
 (the reference syncs with loss.item() every step, trainer.py:556).
 """
 import ctypes
+import itertools
 import os
 import sys
 import time
@@ -46,9 +47,8 @@ def get_trainer(config, dataset, model):
 def eval_keys(eval_data, n_users, n_items):
     """The eval lists as sorted (user * n_items + item) keys plus their lengths:
     what calculate_metrics matches the ranking against (reusable across evals)."""
-    lens = np.array([len(x) for x in eval_data[:n_users]], dtype=np.int32)
-    ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
-    flat = np.fromiter((i for x in eval_data[:n_users] for i in x), dtype=np.int64, count=int(ptr[-1]))
+    ptr, flat = _csr(eval_data, n_users)
+    lens = np.diff(ptr).astype(np.int32)
     return np.unique(np.repeat(np.arange(n_users, dtype=np.int64), lens) * n_items + flat), lens
 
 
@@ -86,9 +86,22 @@ def calculate_metrics(eval_data, rec_items, topks, keys=None):
 
 
 def _csr(lists, n):
-    lens = np.array([len(x) for x in lists[:n]], dtype=np.int64)
-    ptr = np.concatenate([[0], np.cumsum(lens)])
-    flat = np.fromiter((i for x in lists[:n] for i in x), dtype=np.int64, count=int(ptr[-1]))
+    """Per-user lists as (row_ptr, flat items); the iteration runs in C (map / chain)."""
+    lists = lists[:n]
+    lens = np.fromiter(map(len, lists), dtype=np.int64, count=len(lists))
+    ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    flat = np.fromiter(itertools.chain.from_iterable(lists), dtype=np.int64, count=int(ptr[-1]))
+    return ptr, flat
+
+
+def _csr_concat(a, b):
+    """Row-wise concatenation of two CSRs over the same rows: row u = a's items, then b's."""
+    (pa, fa), (pb, fb) = a, b
+    ptr = pa + pb
+    flat = np.empty(len(fa) + len(fb), dtype=np.int64)
+    la, lb = np.diff(pa), np.diff(pb)
+    flat[np.arange(len(fa)) + np.repeat(pb[:-1], la)] = fa
+    flat[np.arange(len(fb)) + np.repeat(pa[1:], lb)] = fb
     return ptr, flat
 
 
@@ -233,10 +246,9 @@ class BasicTrainer:
             cache = self.__dict__.setdefault('_excl', {}) if self.static_eval_lists else {}
             ck = (val_or_test, id(self.dataset.train_data), id(self.dataset.val_data), n_users)
             if ck not in cache:
-                lists = self.dataset.train_data
+                ptr, flat = _csr(self.dataset.train_data, n_users)
                 if val_or_test == 'test':
-                    lists = [a + b for a, b in zip(self.dataset.train_data, self.dataset.val_data)]
-                ptr, flat = _csr(lists, n_users)
+                    ptr, flat = _csr_concat((ptr, flat), _csr(self.dataset.val_data, n_users))
                 cache[ck] = (torch.from_numpy(ptr.astype(np.int64)).to(self.device),
                              torch.from_numpy(flat.astype(np.int32)).to(self.device),
                              self.dataset.train_data, self.dataset.val_data)

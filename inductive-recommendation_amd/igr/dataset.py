@@ -67,9 +67,14 @@ class BasicDataset:
         """dataset.py:133-137."""
         os.makedirs(path, exist_ok=True)
         for name, data in [('train.txt', self.train_data), ('val.txt', self.val_data), ('test.txt', self.test_data)]:
-            with open(os.path.join(path, name), 'w') as f:
-                for user in range(len(data)):
-                    f.write(' '.join([str(user)] + [str(i) for i in data[user]]) + '\n')
+            output_data(os.path.join(path, name), data)
+
+
+def output_data(file_path, data):
+    """dataset.py:40-44: one line per user, 'user item item ...'."""
+    with open(file_path, 'w') as f:
+        for user in range(len(data)):
+            f.write(' '.join([str(user)] + [str(i) for i in data[user]]) + '\n')
 
 
 def read_split(file_path):
@@ -249,6 +254,12 @@ class ProcessedDataset(BasicDataset):
         assert len(self.train_data) == len(self.val_data) == len(self.test_data)
         self.n_users = len(self.train_data)
         self.train_array = [[u, i] for u in range(self.n_users) for i in self.train_data[u]]
+
+    def read_data(self, file_path):
+        """dataset.py:156-164, by its name there: the lists of one split file; n_items grows to cover them."""
+        data, n = read_split(file_path)
+        self.n_items = max(self.n_items, n)
+        return data
 
 
 class AuxiliaryDataset(BasicDataset):

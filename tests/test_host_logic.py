@@ -63,12 +63,25 @@ def test_processed_dataset_roundtrip(tmp_path):
     assert p.val_data == ds.val_data and p.test_data == ds.test_data
 
 
-def test_config_rows_are_on_path():
-    for rows in [C.get_ml_config('cuda'), C.get_gowalla_config('cuda')]:
-        names = {m['name'] for _, m, _ in rows}
-        assert names <= {'LightGCN', 'IGCN', 'IMF', 'NGCF'}
-        igcn = next((m, t) for _, m, t in rows if m['name'] == 'IGCN')
-        assert igcn[0]['dropout'] == 0.3 and igcn[1]['aux_reg'] == 0.01 and igcn[1]['batch_size'] == 2048
+def test_config_tables_match_the_reference_row_by_row():
+    """Every on-path row of the reference's five tables (config.py:1-527), at its index,
+    with its hyper-parameters (tests/golden/make_config_golden.py dumped them); the other
+    rows are None."""
+    import json
+    with open(os.path.join(os.path.dirname(__file__), 'golden', 'config_rows.json')) as f:
+        ref = json.load(f)
+    assert sorted(ref) == ['get_alibaba_config', 'get_amazon_config', 'get_gowalla_config', 'get_ml_config',
+                           'get_yelp_config']
+    for fn, want in ref.items():
+        rows = getattr(C, fn)('DEVICE')
+        assert len(rows) == want['n_rows']
+        for k, row in enumerate(rows):
+            if str(k) in want['rows']:
+                assert [dict(x) for x in row] == want['rows'][str(k)], (fn, k)
+            else:
+                assert row is None, (fn, k)
+    names = [m['name'] for _, m, _ in C.on_path(C.get_ml_config('cuda'))]
+    assert names == ['LightGCN', 'IGCN', 'NGCF', 'IMF']
 
 
 def test_models_need_the_hip_device(golden):

@@ -4,9 +4,8 @@ the hot path.
 `get_{gowalla,yelp,amazon,alibaba,ml}_config(device)` return, as there, a list of
 (dataset_config, model_config, trainer_config) triples with the reference's
 hyper-parameters, and every row sits at the reference's index (scripts pick a
-row by position: [1] LightGCN, [2] IGCN, [4] NGCF, [6] IMF).  Rows whose model
-lies outside this library (MF, ItemKNN, MultiVAE, IMCGAE, IDCF, NeuMF, DOSE) are
-None.  `get_synthetic_config` adds the synthetic benchmark graphs.
+row by position: [1] LightGCN, [2] IGCN, [4] NGCF, [6] IMF, [7] IMCGAE).  Rows whose
+model lies outside this library (MF, ItemKNN, MultiVAE, IDCF, NeuMF, DOSE) are None.  `get_synthetic_config` adds the synthetic benchmark graphs.
 """
 
 TOPKS = [1, 5, 10, 15, 20, 25, 30, 35, 40, 45, 50, 55, 60, 65, 70, 75, 80, 85, 90, 95, 100]
@@ -19,7 +18,8 @@ def _trainer(name, lr, l2_reg, device, **kw):
     return cfg
 
 
-def _table(path, device, n_rows, lgcn_l2=1.e-4, igcn_dropout=0.3, ngcf_dropout=0.1, ngcf_l2=1.e-3, imf_dropout=0.1):
+def _table(path, device, n_rows, lgcn_l2=1.e-4, igcn_dropout=0.3, ngcf_dropout=0.1, ngcf_l2=1.e-3, imf_dropout=0.1,
+           imcgae_dropout=0.3):
     """One dataset's table: the on-path rows at the reference's indices, None elsewhere."""
     ds = {'name': 'ProcessedDataset', 'path': path, 'device': device}
     rows = [None] * n_rows
@@ -35,6 +35,9 @@ def _table(path, device, n_rows, lgcn_l2=1.e-4, igcn_dropout=0.3, ngcf_dropout=0
         rows[6] = (ds, {'name': 'IMF', 'embedding_size': 64, 'n_layers': 0, 'device': device, 'dropout': imf_dropout,
                         'feature_ratio': 1.},
                    _trainer('IGCNTrainer', 1.e-3, 1.e-5, device, aux_reg=0.1))
+    rows[7] = (ds, {'name': 'IMCGAE', 'embedding_size': 64, 'n_layers': 3, 'device': device,
+                    'dropout': imcgae_dropout},
+               _trainer('BPRTrainer', 1.e-3, 0., device))
     return rows
 
 
@@ -51,7 +54,7 @@ def get_yelp_config(device):
 def get_amazon_config(device):
     """config.py:206-290."""
     return _table('data/Amazon/time', device, 11, lgcn_l2=1.e-5, igcn_dropout=0., ngcf_dropout=0.3, ngcf_l2=1.e-4,
-                  imf_dropout=0.3)
+                  imf_dropout=0.3, imcgae_dropout=0.9)
 
 
 def get_alibaba_config(device):

@@ -638,6 +638,81 @@ class AttIGCN(IGCN):
         return users_r, pos_r, neg_r, l2
 
 
+class IMCGAE(BasicModel):
+    """model.py:4300-4345: every node's row is [personal | general | identical]
+    (3 d wide: its own vector, one vector shared by all users or by all items, one
+    shared by everybody); each layer drops nodes at rate dropout - 0.1 i, multiplies
+    by the normalised adjacency, and the layers are summed with weights 1 / (i + 2).
+
+    The reference pushes all 3 d columns through gspmm.  Two of the three blocks are
+    one vector repeated on every row, and A (s g^T) = (A s) g^T: they stay rank one
+    through every layer, so only the personal block takes the d-wide SpMM; the other
+    two follow from one scalar per node and layer (a width-1 product with the same
+    matrix and the same node masks).  Users and items swap general vectors at every
+    layer (the graph is bipartite), which the even / odd sums below account for."""
+
+    def __init__(self, model_config):
+        super().__init__(model_config)
+        self.embedding_size = model_config['embedding_size']
+        self.n_layers = model_config['n_layers']
+        self.dropout = model_config['dropout']
+        self.embedding = nn.Embedding(self.n_users + self.n_items + 3, self.embedding_size)
+        self.norm_adj = self.generate_graph(model_config['dataset'])
+        normal_(self.embedding.weight, std=0.1)
+        self.to(device=self.device)
+
+    def generate_graph(self, dataset):
+        return LightGCN.generate_graph(self, dataset)
+
+    def node_dropout_mask(self, layer):
+        """F.dropout of a vector of ones at rate dropout - 0.1 * layer (model.py:4331-4332),
+        or None when it is the identity.  config['dropout_rng'] = 'cpu' draws it from the
+        CPU generator, as a run of the reference on the CPU does."""
+        p = self.dropout - 0.1 * layer
+        if not self.training or p <= 0:
+            return None
+        n = self.n_users + self.n_items
+        if self.config.get('dropout_rng', 'device') == 'cpu':
+            return F.dropout(torch.ones(n, dtype=torch.float32), p=p, training=True).to(self.device)
+        return F.dropout(torch.ones(n, dtype=torch.float32, device=self.device), p=p, training=True)
+
+    def get_rep(self):
+        U, n = self.n_users, self.n_users + self.n_items
+        w = self.embedding.weight
+        x = w[:n]
+        ident, gen_u, gen_i = w[n], w[n + 1], w[n + 2]
+        s = torch.ones(n, 1, dtype=torch.float32, device=w.device)  # the repeated blocks' scalar per node
+        acc = x
+        even, odd = s, torch.zeros_like(s)  # sums of s_l / (l + 1) over even / odd layers l
+        for i in range(self.n_layers):
+            mask = self.node_dropout_mask(i)
+            if mask is not None:
+                x = x * mask[:, None]
+                s = s * mask[:, None]
+            x = ops.gspmm(self.norm_adj, 'mul', 'sum', x, self.norm_vals)
+            with torch.no_grad():
+                s = ops.gspmm(self.norm_adj, 'mul', 'sum', s, self.norm_vals)
+            acc = acc + x / float(i + 2)
+            if i % 2 == 0:
+                odd = odd + s / float(i + 2)  # layer i + 1
+            else:
+                even = even + s / float(i + 2)
+        # a user's general block: its own side's vector on even layers, the items' on odd ones
+        side = torch.zeros(n, 1, dtype=torch.float32, device=w.device)
+        side[:U] = 1.
+        own = side * gen_u[None, :] + (1. - side) * gen_i[None, :]
+        other = side * gen_i[None, :] + (1. - side) * gen_u[None, :]
+        general = even * own + odd * other
+        identical = (even + odd) * ident[None, :]
+        return torch.cat([acc, general, identical], dim=1)
+
+    def bpr_forward(self, users, pos_items, neg_items):
+        return NGCF.bpr_forward(self, users, pos_items, neg_items)
+
+    def predict(self, users, rep=None):
+        return LightGCN.predict(self, users, rep)
+
+
 def graph_rank_nodes(dataset, ranking_metric):
     """utils.py:186-215 for the 'degree' and 'sort'/'greedy' metrics (feature_ratio < 1)."""
     pairs = train_pairs(dataset)

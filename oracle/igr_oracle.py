@@ -208,6 +208,24 @@ def lightgcn_rep(A, emb, n_layers):
     return np.stack(reps).mean(0).astype(np.float32)
 
 
+def imcgae_rep(A, emb, n_users, n_items, n_layers, masks=None):
+    """IMCGAE.get_rep (model.py:4313-4339) as written there: rows [personal | general |
+    identical] (3 d wide), each layer x <- A (mask_i * x), rep = x_0 + sum_i x_{i+1} / (i + 2).
+    masks: per layer a node-dropout mask (F.dropout of ones) or None (eval mode)."""
+    n = n_users + n_items
+    ident, gen_u, gen_i = emb[n], emb[n + 1], emb[n + 2]
+    x = np.concatenate([np.concatenate([emb[:n_users], np.tile(gen_u, (n_users, 1)), np.tile(ident, (n_users, 1))], 1),
+                        np.concatenate([emb[n_users:n], np.tile(gen_i, (n_items, 1)), np.tile(ident, (n_items, 1))], 1)],
+                       0).astype(np.float32)
+    rep = x.copy()
+    for i in range(n_layers):
+        if masks is not None and masks[i] is not None:
+            x = x * masks[i][:, None]
+        x = spmm(A, x)
+        rep = rep + x / np.float32(i + 2)
+    return rep
+
+
 def igcn_rep(A, F, fvals, emb, n_layers):
     """IGCN.get_rep (model.py:4188-4200) with inductive_rep_layer (4177-4186)."""
     x0 = spmm(F, emb, val=fvals)

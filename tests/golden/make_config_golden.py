@@ -1,6 +1,6 @@
 """Generate tests/golden/config_rows.json from the reference's config tables
 (config.py:1-527): for each of its five getters, the number of rows and the rows
-whose model is on the hot path (LightGCN / IGCN / NGCF / IMF), keyed by their index.
+whose model is on the hot path (LightGCN / IGCN / NGCF / IMF / IMCGAE), keyed by their index.
 
 Run:  python tests/golden/make_config_golden.py
 """
@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, '/root/reference')
 import config as ref_config  # noqa: E402
 
-ON_PATH = {'LightGCN', 'IGCN', 'NGCF', 'IMF'}
+ON_PATH = {'LightGCN', 'IGCN', 'NGCF', 'IMF', 'IMCGAE'}
 
 
 def main():

@@ -81,7 +81,7 @@ def test_config_tables_match_the_reference_row_by_row():
             else:
                 assert row is None, (fn, k)
     names = [m['name'] for _, m, _ in C.on_path(C.get_ml_config('cuda'))]
-    assert names == ['LightGCN', 'IGCN', 'NGCF', 'IMF']
+    assert names == ['LightGCN', 'IGCN', 'NGCF', 'IMF', 'IMCGAE']
 
 
 def test_models_need_the_hip_device(golden):

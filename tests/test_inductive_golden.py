@@ -96,3 +96,22 @@ def test_oracle_inductive_eval_slices(fx):
         for mk in ['Precision', 'Recall', 'NDCG']:
             np.testing.assert_allclose([res[name][mk][k] for k in topks], fx[f'slice{s}_{mk}'], rtol=1e-6,
                                        err_msg=f'{name} {mk}')
+
+
+def test_oracle_imcgae_rep():
+    """IMCGAE.get_rep (model.py:4313-4339) restated in the oracle against the reference run
+    (tests/golden/make_imcgae_golden.py), eval mode and train mode - the train-mode masks are
+    the draws F.dropout makes from the CPU generator at the fixture's seed."""
+    import torch
+    import torch.nn.functional as F
+    with np.load(os.path.join(GOLDEN, 'imcgae.npz')) as z:
+        g = {k: z[k] for k in z.files}
+    L, p = int(g['n_layers']), float(g['dropout'])
+    for cname in ['uni', 'pow']:
+        with np.load(os.path.join(GOLDEN, cname + '.npz')) as z:
+            nu, ni, ta = int(z['n_users']), int(z['n_items']), z['train_array']
+        A = O.norm_adj(nu, ni, ta)
+        close(O.imcgae_rep(A, g[cname + '_emb'], nu, ni, L), g[cname + '_rep'])
+        torch.manual_seed(int(g['train_seed']))
+        masks = [F.dropout(torch.ones(nu + ni), p=p - 0.1 * i, training=True).numpy() for i in range(L)]
+        close(O.imcgae_rep(A, g[cname + '_emb'], nu, ni, L, masks), g[cname + '_train_rep'])

@@ -108,6 +108,36 @@ def plan(row_ptr, split_threshold=DEFAULT_SPLIT_THRESHOLD, chunk_edges=DEFAULT_C
                 chunk_row=chunk_row[:nc.value], chunk_beg=chunk_beg[:nc.value], chunk_edges=chunk_edges)
 
 
+# Row-plan choice for small graphs.  On a graph whose rows all run at once (a few thousand to
+# a few tens of thousands of rows) an SpMM lasts as long as its longest unsplit row: one
+# 16-lane group walks that row 16 edges per round, ~1.6 us a round on MI355X, while the
+# split rows' chunks (one wave each) and the combine pass cost a few us in total.  The
+# estimate below was fitted to measured launches (ML-100K / ML-1M shapes, uniform and
+# MovieLens-like item popularity, 7 thresholds each; scripts/tune_small_plan.py) and is
+# evaluated on the degree array alone, so a graph always gets the same plan.
+AUTO_PLAN_MAX_NNZ = 4_000_000  # larger graphs are throughput-bound: the default plan
+_PLAN_THRESHOLDS = (512, 384, 256, 192, 128, 96, 64)
+
+
+def auto_plan(row_ptr):
+    """(split_threshold, chunk_edges) for this degree distribution."""
+    deg = np.diff(_np(row_ptr, np.int64))
+    if len(deg) == 0 or int(row_ptr[-1]) > AUTO_PLAN_MAX_NNZ or int(deg.max()) <= _PLAN_THRESHOLDS[-1]:
+        return DEFAULT_SPLIT_THRESHOLD, DEFAULT_CHUNK_EDGES
+    best = None
+    for t in _PLAN_THRESHOLDS:  # ties go to the larger threshold (fewer split rows)
+        c = min(2 * t, DEFAULT_CHUNK_EDGES)
+        fast, split = deg[deg <= t], deg[deg > t]
+        rounds = -(-int(fast.max()) // 16) if fast.size else 0
+        chunk_rounds = -(-min(c, int(split.max())) // 64) if split.size else 0
+        est = max(1.57 * rounds, 16.1e-6 * float(fast.sum()), 0.8 * chunk_rounds)
+        if split.size:
+            est += 3.29e-6 * float(split.sum()) + 1.96e-3 * split.size + 0.38e-3 * float((-(-split // c)).sum()) + 2.8
+        if best is None or est < best[0]:
+            best = (est, t, c)
+    return best[1], best[2]
+
+
 # ------------------------------------------------------------------ Graph
 
 class Graph:
@@ -118,9 +148,15 @@ class Graph:
     unsorted edge list)."""
 
     def __init__(self, row_ptr, col_idx, n_rows, n_cols, device='cuda', edge_id=None, symmetric=False,
-                 split_threshold=DEFAULT_SPLIT_THRESHOLD, chunk_edges=DEFAULT_CHUNK_EDGES, window=None):
+                 split_threshold=None, chunk_edges=None, window=None):
         row_ptr = _np(row_ptr, np.int64)
         col_idx = _np(col_idx, np.int32)
+        # no plan given: chosen from the degree distribution (auto_plan)
+        self._auto_plan = split_threshold is None and chunk_edges is None
+        if self._auto_plan:
+            split_threshold, chunk_edges = auto_plan(row_ptr)
+        split_threshold = DEFAULT_SPLIT_THRESHOLD if split_threshold is None else split_threshold
+        chunk_edges = DEFAULT_CHUNK_EDGES if chunk_edges is None else chunk_edges
         self.n_rows, self.n_cols = int(n_rows), int(n_cols)
         assert len(row_ptr) == self.n_rows + 1, 'row_ptr must have n_rows + 1 entries'
         self.nnz = int(row_ptr[-1])
@@ -186,8 +222,8 @@ class Graph:
             h = self._host
             t_rp, t_ci, t_pos = csr_transpose(h['row_ptr'], h['col_idx'], self.n_rows, self.n_cols)
             eid = t_pos if h['edge_id'] is None else h['edge_id'][t_pos]
-            self._reverse = Graph(t_rp, t_ci, self.n_cols, self.n_rows, device=self.device, edge_id=eid,
-                                  split_threshold=self.split_threshold, chunk_edges=self.chunk_edges)
+            own = {} if self._auto_plan else dict(split_threshold=self.split_threshold, chunk_edges=self.chunk_edges)
+            self._reverse = Graph(t_rp, t_ci, self.n_cols, self.n_rows, device=self.device, edge_id=eid, **own)
             self._reverse._reverse = self
         return self._reverse
 

@@ -31,13 +31,27 @@ def timeit(fn, reps=200):
     return a.elapsed_time(b) / reps * 1e3
 
 
+def skewed_pairs(shape):
+    """The MovieLens-shaped (skewed item popularity) training pairs of the parity tests."""
+    sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
+    import ml_like
+    nu, ni, mean_deg, d, _L, _ = ml_like.SHAPES[shape]
+    train, _, _ = ml_like.make_splits(nu, ni, mean_deg, seed=100)
+    return nu, ni, d, np.array([[u, i] for u in range(nu) for i in train[u]], dtype=np.int64)
+
+
 def main():
     from igr import graph as G, ops
     from igr.dataset import synthetic_pairs
     dev = torch.device('cuda')
     out = {}
-    for name, (U, I, E, d) in SHAPES.items():
-        pairs = synthetic_pairs(U, I, E, 0)
+    cases = {name: (U, I, d, synthetic_pairs(U, I, E, 0)) for name, (U, I, E, d) in SHAPES.items()}
+    if '--skewed' in sys.argv:
+        cases.update({'ml1m_skewed': skewed_pairs('ml1m_l3'), 'ml100k_skewed': skewed_pairs('ml100k'),
+                      'gowalla_skewed': skewed_pairs('gowalla')})
+        PLANS.extend([(256, 256), (128, 128), (128, 256), (256, 512), (64, 64), (64, 128), (384, 384), (192, 192),
+                      (384, 512), (192, 384), (96, 192)])
+    for name, (U, I, d, pairs) in cases.items():
         row = np.concatenate([pairs[:, 0], U + pairs[:, 1]])
         col = np.concatenate([U + pairs[:, 1], pairs[:, 0]])
         x = torch.randn(U + I, d, device=dev) * 0.1

@@ -90,7 +90,7 @@ def test_sharded_world1_equals_igcn_trainer(batch_rep):
     m.train()
     for s in range(STEPS):
         loss = tr.step(*(torch.from_numpy(a).to(DEV) for a in bl[s]))
-        assert float(loss) == pytest.approx(ref_losses[s], rel=1e-5)
+        assert float(loss.detach()) == pytest.approx(ref_losses[s], rel=1e-5)
     np.testing.assert_allclose(m.embedding.weight.detach().cpu().numpy(), ref_emb, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(m.w.detach().cpu().numpy(), ref_w, rtol=1e-5, atol=1e-6)
 

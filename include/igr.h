@@ -314,6 +314,15 @@ int igr_sddmm_shared_f32(const igr_csr *g, int32_t h, int32_t d, const float *u,
                          const float *v, int64_t ld_v, float *out, void *stream);
 int igr_spmm_shared_heads_f32(const igr_csr *g, int32_t h, int32_t d, const float *x, int64_t ldx,
                               const float *rhs, float *y, int64_t ldy, void *stream);
+/* The same with a workspace for the partial sums of split rows (the graph's schedule cuts
+ * rows longer than its threshold into chunks, one wave each; a hub row - an item most users
+ * rated - is otherwise one wave's serial loop): igr_spmm_shared_heads_workspace_size bytes,
+ * 16-byte aligned; NULL = every row by one wave, as igr_spmm_shared_heads_f32.  A row's
+ * chunk partials are added in chunk order (deterministic). */
+int64_t igr_spmm_shared_heads_workspace_size(const igr_csr *g, int32_t h, int32_t d);
+int igr_spmm_shared_heads_ws_f32(const igr_csr *g, int32_t h, int32_t d, const float *x, int64_t ldx,
+                                 const float *rhs, float *y, int64_t ldy, float *workspace,
+                                 int64_t workspace_bytes, void *stream);
 
 /* gspmm(g, 'copy_rhs', 'sum'|'max', None, x): out[r, h] = reduce over edges
  * of row r of x[eid, h]; empty rows give 0 (model.py:4270, 4273).

@@ -116,16 +116,33 @@ struct SddmmShared {
     }
 };
 
-template <int D, int H, bool EID>
+template <int D, int H, bool EID, bool PLAN>
 __global__ __launch_bounds__(256) void sddmm_shared_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr,
                                                            const int32_t *__restrict__ col,
-                                                           const int64_t *__restrict__ eid,
+                                                           const int64_t *__restrict__ eid, RowPlan plan,
                                                            const float *__restrict__ u, int64_t ld_u,
                                                            const float *__restrict__ v, int ld_v,
                                                            float *__restrict__ out) {
     using S = SddmmShared<D, H, EID>;
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= n_rows) return;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    int64_t r, b, e;
+    if (PLAN) {
+        if (w >= plan.n_chunks + plan.n_order) return;
+        if (w < plan.n_chunks) {
+            r = plan.chunk_row[w];
+            b = plan.chunk_beg[w];
+            e = min(b + plan.chunk_edges, row_ptr[r + 1]);
+        } else {
+            r = plan.order[w - plan.n_chunks];
+            b = row_ptr[r];
+            e = row_ptr[r + 1];
+        }
+    } else {
+        r = w;
+        if (r >= n_rows) return;
+        b = row_ptr[r];
+        e = row_ptr[r + 1];
+    }
     const int lane = threadIdx.x & 63;
     const int eg = lane / S::LPE;
     const int sub = lane - eg * S::LPE;
@@ -133,7 +150,6 @@ __global__ __launch_bounds__(256) void sddmm_shared_kernel(int64_t n_rows, const
 #pragma unroll
     for (int hh = 0; hh < H; ++hh) uq[hh] = *reinterpret_cast<const v4f *>(u + r * ld_u + hh * D + sub * 4);
     const float *vs = v + sub * 4;
-    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
     for (int64_t base = b; base < e; base += 64) {
         const int n = (int)min((int64_t)64, e - base);
         const int cl = lane < n ? col[base + lane] : 0;
@@ -163,19 +179,43 @@ __global__ __launch_bounds__(256) void sddmm_shared_kernel(int64_t n_rows, const
 // y[r, hh, :] = sum over the edges of row r of rhs[eid, hh] * x[col, :]: each source row
 // is gathered once and feeds H accumulators; the EPW lane groups take alternate edges
 // and are summed in a fixed xor tree at the end (deterministic).
-template <int D, int H>
+// With a row plan (PLAN) a wave takes one chunk of a split row, whose partial sums go to
+// its slot of `ws` (H * D floats per chunk; heads_combine_kernel adds a row's slots in
+// chunk order), or one whole unsplit row, heaviest first.
+template <int D, int H, bool PLAN>
 __global__ __launch_bounds__(256) void spmm_shared_heads_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr,
                                                                 const int32_t *__restrict__ col,
-                                                                const int64_t *__restrict__ eid,
+                                                                const int64_t *__restrict__ eid, RowPlan plan,
                                                                 const float *__restrict__ x, int ldx,
                                                                 const float *__restrict__ rhs,
-                                                                float *__restrict__ y, int64_t ldy) {
+                                                                float *__restrict__ y, int64_t ldy,
+                                                                float *__restrict__ ws) {
     constexpr int LPE = D / 4;
     constexpr int EPW = 64 / LPE;
     constexpr int UE = IGR_SPMM_SHARED_U;
     constexpr int TRIP = UE * EPW;
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= n_rows) return;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    int64_t b, e;
+    float *dst;
+    if (PLAN) {
+        if (w >= plan.n_chunks + plan.n_order) return;
+        if (w < plan.n_chunks) {
+            const int64_t r = plan.chunk_row[w];
+            b = plan.chunk_beg[w];
+            e = min(b + plan.chunk_edges, row_ptr[r + 1]);
+            dst = ws + w * (int64_t)(H * D);
+        } else {
+            const int64_t r = plan.order[w - plan.n_chunks];
+            b = row_ptr[r];
+            e = row_ptr[r + 1];
+            dst = y + r * ldy;
+        }
+    } else {
+        if (w >= n_rows) return;
+        b = row_ptr[w];
+        e = row_ptr[w + 1];
+        dst = y + w * ldy;
+    }
     const int lane = threadIdx.x & 63;
     const int eg = lane / LPE;
     const int sub = lane - eg * LPE;
@@ -183,7 +223,6 @@ __global__ __launch_bounds__(256) void spmm_shared_heads_kernel(int64_t n_rows, 
     float4 acc[H];
 #pragma unroll
     for (int hh = 0; hh < H; ++hh) acc[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
     for (int64_t base = b; base < e; base += 64) {
         const int n = (int)min((int64_t)64, e - base);
         const int cl = lane < n ? col[base + lane] : 0;
@@ -235,8 +274,28 @@ __global__ __launch_bounds__(256) void spmm_shared_heads_kernel(int64_t n_rows, 
         }
     if (eg == 0) {
 #pragma unroll
-        for (int hh = 0; hh < H; ++hh) *reinterpret_cast<float4 *>(y + r * ldy + hh * D + sub * 4) = acc[hh];
+        for (int hh = 0; hh < H; ++hh) *reinterpret_cast<float4 *>(dst + hh * D + sub * 4) = acc[hh];
     }
+}
+
+// y[split_row[s], :] = the sum of the row's chunk partials, in chunk order (one block per
+// split row, one float4 column group per thread; width = H * D floats <= 512).
+__global__ __launch_bounds__(128) void heads_combine_kernel(int64_t n_split, const int32_t *__restrict__ split_row,
+                                                            const int64_t *__restrict__ split_ptr,
+                                                            const float *__restrict__ ws, int width,
+                                                            float *__restrict__ y, int64_t ldy) {
+    const int64_t s = blockIdx.x;
+    const int t = threadIdx.x * 4;
+    if (s >= n_split || t >= width) return;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t k = split_ptr[s]; k < split_ptr[s + 1]; ++k) {
+        const float4 p = *reinterpret_cast<const float4 *>(ws + k * width + t);
+        acc.x += p.x;
+        acc.y += p.y;
+        acc.z += p.z;
+        acc.w += p.w;
+    }
+    *reinterpret_cast<float4 *>(y + (int64_t)split_row[s] * ldy + t) = acc;
 }
 
 template <template <int, int> class Launch, class... Args>
@@ -254,22 +313,43 @@ template <int D, int H>
 struct LaunchSddmmShared {
     static void go(const igr_csr *g, const float *u, int64_t ld_u, const float *v, int64_t ld_v, float *out,
                    hipStream_t st) {
-        const dim3 grid((unsigned)((g->n_rows + 3) / 4));
-        if (g->edge_id)
-            hipLaunchKernelGGL((sddmm_shared_kernel<D, H, true>), grid, dim3(256), 0, st, g->n_rows, g->row_ptr,
-                               g->col_idx, g->edge_id, u, ld_u, v, (int)ld_v, out);
-        else
-            hipLaunchKernelGGL((sddmm_shared_kernel<D, H, false>), grid, dim3(256), 0, st, g->n_rows, g->row_ptr,
-                               g->col_idx, g->edge_id, u, ld_u, v, (int)ld_v, out);
+        const RowPlan plan = row_plan_of(g);
+        const bool planned = use_row_plan(g);
+        const int64_t waves = planned ? g->n_chunks + g->n_order : g->n_rows;
+        const dim3 grid((unsigned)((waves + 3) / 4));
+#define IGR_GO(EID_, PLAN_)                                                                                    \
+    hipLaunchKernelGGL((sddmm_shared_kernel<D, H, EID_, PLAN_>), grid, dim3(256), 0, st, g->n_rows, g->row_ptr, \
+                       g->col_idx, g->edge_id, plan, u, ld_u, v, (int)ld_v, out)
+        if (g->edge_id) {
+            if (planned) IGR_GO(true, true);
+            else IGR_GO(true, false);
+        } else {
+            if (planned) IGR_GO(false, true);
+            else IGR_GO(false, false);
+        }
+#undef IGR_GO
     }
 };
 
 template <int D, int H>
 struct LaunchSpmmShared {
     static void go(const igr_csr *g, const float *x, int64_t ldx, const float *rhs, float *y, int64_t ldy,
-                   hipStream_t st) {
-        hipLaunchKernelGGL((spmm_shared_heads_kernel<D, H>), dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0, st,
-                           g->n_rows, g->row_ptr, g->col_idx, g->edge_id, x, (int)ldx, rhs, y, ldy);
+                   float *ws, hipStream_t st) {
+        const RowPlan plan = row_plan_of(g);
+        // split rows need the workspace for their chunk partials; without one every row is one wave's
+        const bool planned = use_row_plan(g) && (g->n_chunks == 0 || ws != nullptr);
+        const int64_t waves = planned ? g->n_chunks + g->n_order : g->n_rows;
+        const dim3 grid((unsigned)((waves + 3) / 4));
+        if (planned) {
+            hipLaunchKernelGGL((spmm_shared_heads_kernel<D, H, true>), grid, dim3(256), 0, st, g->n_rows, g->row_ptr,
+                               g->col_idx, g->edge_id, plan, x, (int)ldx, rhs, y, ldy, ws);
+            if (g->n_split > 0)
+                hipLaunchKernelGGL(heads_combine_kernel, dim3((unsigned)g->n_split), dim3(128), 0, st, g->n_split,
+                                   g->split_row, g->split_ptr, ws, H * D, y, ldy);
+        } else {
+            hipLaunchKernelGGL((spmm_shared_heads_kernel<D, H, false>), grid, dim3(256), 0, st, g->n_rows, g->row_ptr,
+                               g->col_idx, g->edge_id, plan, x, (int)ldx, rhs, y, ldy, ws);
+        }
     }
 };
 
@@ -297,8 +377,22 @@ extern "C" int igr_sddmm_shared_f32(const igr_csr *g, int32_t h, int32_t d, cons
 
 extern "C" int igr_spmm_shared_heads_f32(const igr_csr *g, int32_t h, int32_t d, const float *x, int64_t ldx,
                                          const float *rhs, float *y, int64_t ldy, void *stream) {
-    return guarded("igr_spmm_shared_heads_f32", [&]() -> int {
-        const char *fn = "igr_spmm_shared_heads_f32";
+    return igr_spmm_shared_heads_ws_f32(g, h, d, x, ldx, rhs, y, ldy, nullptr, 0, stream);
+}
+
+extern "C" int64_t igr_spmm_shared_heads_workspace_size(const igr_csr *g, int32_t h, int32_t d) {
+    if (!g || h <= 0 || d <= 0 || g->n_chunks <= 0) return 0;
+    return g->n_chunks * (int64_t)h * d * (int64_t)sizeof(float);
+}
+
+extern "C" int igr_spmm_shared_heads_ws_f32(const igr_csr *g, int32_t h, int32_t d, const float *x, int64_t ldx,
+                                            const float *rhs, float *y, int64_t ldy, float *workspace,
+                                            int64_t workspace_bytes, void *stream) {
+    return guarded("igr_spmm_shared_heads_ws_f32", [&]() -> int {
+        const char *fn = "igr_spmm_shared_heads_ws_f32";
+        if (workspace && g && workspace_bytes < igr_spmm_shared_heads_workspace_size(g, h, d))
+            return arg_error(fn, "workspace smaller than igr_spmm_shared_heads_workspace_size");
+        if (workspace && !aligned16(workspace)) return arg_error(fn, "workspace must be 16-byte aligned");
         if (!g || h <= 0 || d <= 0) return arg_error(fn, "bad graph / h / d");
         if (ldx < d || ldy < (int64_t)h * d) return arg_error(fn, "leading dimension too small");
         if (g->n_rows == 0) return IGR_OK;
@@ -307,7 +401,8 @@ extern "C" int igr_spmm_shared_heads_f32(const igr_csr *g, int32_t h, int32_t d,
             return arg_error(fn, "x / y must be 16-byte aligned with leading dimensions a multiple of 4");
         if (ldx > 2147483647) return arg_error(fn, "ldx too large");
         if (h % 4 == 0 && g->nnz > 0 && !aligned16(rhs)) return arg_error(fn, "rhs must be 16-byte aligned");
-        if (!dispatch_dh<LaunchSpmmShared>(d, h, g, x, ldx, rhs, y, ldy, reinterpret_cast<hipStream_t>(stream)))
+        if (!dispatch_dh<LaunchSpmmShared>(d, h, g, x, ldx, rhs, y, ldy, workspace,
+                                           reinterpret_cast<hipStream_t>(stream)))
             return arg_error(fn, "supported: d in {32, 64, 128, 256} with h * d <= 512, h a power of two");
         return launch_status(fn);
     });

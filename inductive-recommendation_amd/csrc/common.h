@@ -45,6 +45,40 @@ inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 constexpr int kWave = 64;  // CDNA wavefront
 
+// The row schedule of a graph as the per-edge kernels use it (scores, dropout draws: an
+// edge's result depends on no other edge, so the chunks of a split row need no combining):
+// a wave takes one chunk of a split row or one whole unsplit row, heaviest first.
+struct RowPlan {
+    int64_t n_chunks;
+    const int32_t *chunk_row;
+    const int64_t *chunk_beg;
+    int64_t chunk_edges;
+    int64_t n_order;
+    const int32_t *order;
+};
+
+inline RowPlan row_plan_of(const igr_csr *g) {
+    return RowPlan{g->n_chunks, g->chunk_row, g->chunk_beg, g->chunk_edges, g->n_order, g->order};
+}
+
+// A graph carries a usable schedule when its unsplit-row list and its chunk list are both
+// there (igr_plan_fill) and cover something.
+inline bool has_row_plan(const igr_csr *g) {
+    if (g->n_order + g->n_chunks <= 0) return false;
+    if (g->n_order > 0 && !g->order) return false;
+    if (g->n_chunks > 0 && (!g->chunk_row || !g->chunk_beg || g->chunk_edges <= 0)) return false;
+    return true;
+}
+
+// The plan is used where it pays: when rows were split (skewed degrees: a hub row would
+// otherwise be one wave's serial loop) or when the graph is small enough for a launch to
+// last as long as its heaviest row (heaviest first).  On a large graph of alike rows the
+// natural row order streams the per-row operands better (SDDMM at nnz 411 M, h = 4,
+// d = 64: 19.8 ms against 20.4).
+inline bool use_row_plan(const igr_csr *g) {
+    return has_row_plan(g) && (g->n_chunks > 0 || g->n_rows <= (1 << 18));
+}
+
 }  // namespace igr
 
 // ---------------------------------------------------------------- device helpers

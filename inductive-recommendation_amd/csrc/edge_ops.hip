@@ -300,10 +300,13 @@ template <int H, int R, int LPR>
 __global__ __launch_bounds__(256) void att_softmax_g16_kernel(
     int64_t n_rows, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
     const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d, float *__restrict__ w,
-    float *__restrict__ row_max, float *__restrict__ row_sum) {
-    const int64_t r = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
+    float *__restrict__ row_max, float *__restrict__ row_sum, const int32_t *__restrict__ order) {
+    // n_rows rows, or with `order` the n_rows rows it lists (the unsplit rows of the graph's
+    // schedule, heaviest first; att_softmax_block_kernel takes the split ones)
+    const int64_t idx = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
     const int sub = threadIdx.x % LPR;
-    const bool live = r < n_rows;  // every lane stays for the group shuffles
+    const bool live = idx < n_rows;  // every lane stays for the group shuffles
+    const int64_t r = live ? (order ? (int64_t)order[idx] : idx) : 0;
     const int64_t b = live ? row_ptr[r] : 0, e = live ? row_ptr[r + 1] : 0;
     float a[R][H];
     bool k[R];
@@ -397,10 +400,12 @@ template <int H, int R, int LPR>
 __global__ __launch_bounds__(256) void att_softmax_bwd_g16_kernel(
     int64_t n_rows, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
     const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d, const float *__restrict__ row_max,
-    const float *__restrict__ row_sum, const float *__restrict__ dw, float *__restrict__ dalpha) {
-    const int64_t r = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
+    const float *__restrict__ row_sum, const float *__restrict__ dw, float *__restrict__ dalpha,
+    const int32_t *__restrict__ order) {
+    const int64_t idx = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
     const int sub = threadIdx.x % LPR;
-    const bool live = r < n_rows;
+    const bool live = idx < n_rows;
+    const int64_t r = live ? (order ? (int64_t)order[idx] : idx) : 0;
     const int64_t b = live ? row_ptr[r] : 0, e = live ? row_ptr[r + 1] : 0;
     float m[H], s[H], S[H];
 #pragma unroll
@@ -461,6 +466,207 @@ __global__ __launch_bounds__(256) void att_softmax_bwd_g16_kernel(
         if (kk) load_heads<H>(alpha, ed, x);
 #pragma unroll
         for (int j = 0; j < H; ++j) dalpha[ed * H + j] = kk ? att_exp(x[j], m[j], sqrt_d) / s[j] * (gg - S[j]) / c : 0.f;
+    }
+}
+
+// ---------------------------------------------------------------- split rows: a workgroup per row
+// A hub row (an item most users rated, a general-feature row) is thousands of edges long:
+// as one lane group's loop it outlasts the rest of the launch.  The rows the graph's
+// schedule splits (degree above its threshold) go to these kernels instead, a whole
+// workgroup each: per-thread partials over a strided walk of the row, a fixed xor tree
+// inside each wave, then the waves' results combined in wave order through LDS - the
+// same value in every thread, the same bits on every run.  (MovieLens-1M-shaped feature
+// graph, 4 heads, no register cache: 31.5 us at 512 threads, 38.4 at 256, 72.8 at 1024; a
+// wave each for the split rows up to 1024 edges and workgroups for the longer ones: 63 us.)
+// Also tried: a wave each for the split rows up to 256 edges (whole row in registers) and
+// workgroups for the longer ones only - forward 37 us against 38, backward 43 against 37.
+#ifndef IGR_SOFTMAX_BLOCK_R
+#define IGR_SOFTMAX_BLOCK_R 4
+#endif
+constexpr int kSoftmaxBlockR = IGR_SOFTMAX_BLOCK_R;  // register-cached edges per thread
+#ifndef IGR_SOFTMAX_BLOCK
+#define IGR_SOFTMAX_BLOCK 512
+#endif
+constexpr int kSoftmaxBlock = IGR_SOFTMAX_BLOCK;
+
+template <int H, int NT, bool MAX>
+__device__ __forceinline__ void block_reduce(float (&v)[H], float (*red)[H]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < H; ++j) v[j] = MAX ? gmax<64>(v[j]) : gsum<64>(v[j]);
+    __syncthreads();  // red may still be read from the previous reduction
+    if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) red[wave][j] = v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        float a = red[0][j];
+#pragma unroll
+        for (int k = 1; k < NT / 64; ++k) a = MAX ? fmaxf(a, red[k][j]) : a + red[k][j];
+        v[j] = a;
+    }
+}
+
+template <int H, int NT, int R>
+__global__ __launch_bounds__(NT) void att_softmax_block_kernel(
+    int64_t n_split, const int32_t *__restrict__ split_row, const int64_t *__restrict__ row_ptr,
+    const int64_t *__restrict__ eid, const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d,
+    float *__restrict__ w, float *__restrict__ row_max, float *__restrict__ row_sum) {
+    __shared__ float red[NT / 64][H];
+    const int64_t r = split_row[blockIdx.x];
+    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
+    // the first NT * R edges of the row stay in registers (one read of alpha, all of a
+    // thread's loads in flight together); a longer row re-reads its tail in every pass
+    float a[R][H], m[H], sm[H];
+    int64_t ed[R];
+    bool k[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const int64_t p = b + threadIdx.x + (int64_t)NT * t;
+        ed[t] = p < e ? (eid ? eid[p] : p) : -1;
+    }
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        k[t] = ed[t] >= 0 && kept(keep, ed[t]);
+        if (k[t]) load_heads<H>(alpha, ed[t], a[t]);
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) m[j] = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+        if (k[t]) {
+#pragma unroll
+            for (int j = 0; j < H; ++j) m[j] = fmaxf(m[j], a[t][j]);
+        }
+    for (int64_t p = b + threadIdx.x + (int64_t)NT * R; p < e; p += NT) {
+        const int64_t ee = eid ? eid[p] : p;
+        if (!kept(keep, ee)) continue;
+        float x[H];
+        load_heads<H>(alpha, ee, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) m[j] = fmaxf(m[j], x[j]);
+    }
+    block_reduce<H, NT, true>(m, red);
+#pragma unroll
+    for (int j = 0; j < H; ++j) sm[j] = 0.f;
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+        if (k[t]) {
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                a[t][j] = att_exp(a[t][j], m[j], sqrt_d);
+                sm[j] += a[t][j];
+            }
+        }
+    for (int64_t p = b + threadIdx.x + (int64_t)NT * R; p < e; p += NT) {
+        const int64_t ee = eid ? eid[p] : p;
+        if (!kept(keep, ee)) continue;
+        float x[H];
+        load_heads<H>(alpha, ee, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) sm[j] += att_exp(x[j], m[j], sqrt_d);
+    }
+    block_reduce<H, NT, false>(sm, red);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            if (row_max) row_max[r * H + j] = m[j];
+            if (row_sum) row_sum[r * H + j] = sm[j];
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+        if (ed[t] >= 0) {
+            float acc = 0.f;
+            if (k[t]) {
+#pragma unroll
+                for (int j = 0; j < H; ++j) acc += a[t][j] / sm[j];
+                acc /= (float)H;
+            }
+            w[ed[t]] = acc;
+        }
+    for (int64_t p = b + threadIdx.x + (int64_t)NT * R; p < e; p += NT) {
+        const int64_t ee = eid ? eid[p] : p;
+        if (!kept(keep, ee)) {
+            w[ee] = 0.f;
+            continue;
+        }
+        float x[H];
+        load_heads<H>(alpha, ee, x);
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < H; ++j) acc += att_exp(x[j], m[j], sqrt_d) / sm[j];
+        w[ee] = acc / (float)H;
+    }
+}
+
+template <int H, int NT, int R>
+__global__ __launch_bounds__(NT) void att_softmax_bwd_block_kernel(
+    int64_t n_split, const int32_t *__restrict__ split_row, const int64_t *__restrict__ row_ptr,
+    const int64_t *__restrict__ eid, const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d,
+    const float *__restrict__ row_max, const float *__restrict__ row_sum, const float *__restrict__ dw,
+    float *__restrict__ dalpha) {
+    __shared__ float red[NT / 64][H];
+    const int64_t r = split_row[blockIdx.x];
+    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
+    float m[H], s[H], S[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        m[j] = row_max[r * H + j];
+        s[j] = row_sum[r * H + j];
+        S[j] = 0.f;
+    }
+    const float inv_h = 1.f / (float)H;
+    float a[R][H], g[R];
+    int64_t ed[R];
+    bool k[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const int64_t p = b + threadIdx.x + (int64_t)NT * t;
+        ed[t] = p < e ? (eid ? eid[p] : p) : -1;
+    }
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        k[t] = ed[t] >= 0 && kept(keep, ed[t]);
+        g[t] = ed[t] >= 0 ? dw[ed[t]] * inv_h : 0.f;
+        if (k[t]) load_heads<H>(alpha, ed[t], a[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+        if (k[t]) {
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                a[t][j] = att_exp(a[t][j], m[j], sqrt_d) / s[j];
+                S[j] += a[t][j] * g[t];
+            }
+        }
+    for (int64_t p = b + threadIdx.x + (int64_t)NT * R; p < e; p += NT) {
+        const int64_t ee = eid ? eid[p] : p;
+        if (!kept(keep, ee)) continue;
+        const float gg = dw[ee] * inv_h;
+        float x[H];
+        load_heads<H>(alpha, ee, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) S[j] += att_exp(x[j], m[j], sqrt_d) / s[j] * gg;
+    }
+    block_reduce<H, NT, false>(S, red);
+    const float c = sqrt_d * 10.f;
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+        if (ed[t] >= 0) {
+#pragma unroll
+            for (int j = 0; j < H; ++j) dalpha[ed[t] * H + j] = k[t] ? a[t][j] * (g[t] - S[j]) / c : 0.f;
+        }
+    for (int64_t p = b + threadIdx.x + (int64_t)NT * R; p < e; p += NT) {
+        const int64_t ee = eid ? eid[p] : p;
+        const bool kk = kept(keep, ee);
+        const float gg = dw[ee] * inv_h;
+        float x[H];
+        if (kk) load_heads<H>(alpha, ee, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) dalpha[ee * H + j] = kk ? att_exp(x[j], m[j], sqrt_d) / s[j] * (gg - S[j]) / c : 0.f;
     }
 }
 
@@ -535,6 +741,12 @@ static bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 #define IGR_WIDE_ROW_DEG 96
 #endif
 static bool wide_rows(const igr_csr *g) { return g->nnz >= (int64_t)IGR_WIDE_ROW_DEG * g->n_rows; }
+
+// The graph's schedule lists its unsplit rows (order) and its split rows (split_row), and
+// some row is split: the row kernels then take the two lists separately.
+static bool split_plan(const igr_csr *g) {
+    return g->n_split > 0 && g->split_row && (g->n_order == 0 || g->order) && g->n_order + g->n_split == g->n_rows;
+}
 
 struct SddmmArgs {
     const igr_csr *g;
@@ -653,20 +865,33 @@ extern "C" int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alp
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         const bool wide = wide_rows(g);
-        const dim3 g16((unsigned)((g->n_rows + 15) / 16)), g64((unsigned)((g->n_rows + 3) / 4));
+        // with a schedule that splits rows: the unsplit rows by lane groups, heaviest first,
+        // and every split row by a workgroup of its own
+        const bool planned = split_plan(g);
+        const int64_t nr = planned ? g->n_order : g->n_rows;
+        const int32_t *order = planned ? g->order : nullptr;
+        const dim3 g16((unsigned)((nr + 15) / 16)), g64((unsigned)((nr + 3) / 4));
         const bool vec = (reinterpret_cast<uintptr_t>(alpha) & 15u) == 0;
 #define IGR_SM(HH, RR)                                                                                            \
-    if (wide)                                                                                                     \
-        hipLaunchKernelGGL((att_softmax_g16_kernel<HH, RR, 64>), g64, dim3(256), 0, st, g->n_rows, g->row_ptr,   \
-                           g->edge_id, alpha, keep, sqrt_d, w, row_max, row_sum);                                 \
-    else                                                                                                          \
-        hipLaunchKernelGGL((att_softmax_g16_kernel<HH, RR, 16>), g16, dim3(256), 0, st, g->n_rows, g->row_ptr,   \
-                           g->edge_id, alpha, keep, sqrt_d, w, row_max, row_sum)
+    do {                                                                                                          \
+        if (nr > 0) {                                                                                             \
+            if (wide)                                                                                             \
+                hipLaunchKernelGGL((att_softmax_g16_kernel<HH, RR, 64>), g64, dim3(256), 0, st, nr, g->row_ptr,  \
+                                   g->edge_id, alpha, keep, sqrt_d, w, row_max, row_sum, order);                 \
+            else                                                                                                  \
+                hipLaunchKernelGGL((att_softmax_g16_kernel<HH, RR, 16>), g16, dim3(256), 0, st, nr, g->row_ptr,  \
+                                   g->edge_id, alpha, keep, sqrt_d, w, row_max, row_sum, order);                 \
+        }                                                                                                         \
+        if (planned)                                                                                              \
+            hipLaunchKernelGGL((att_softmax_block_kernel<HH, kSoftmaxBlock, kSoftmaxBlockR>),                     \
+                               dim3((unsigned)g->n_split), dim3(kSoftmaxBlock), 0, st, g->n_split, g->split_row,  \
+                               g->row_ptr, g->edge_id, alpha, keep, sqrt_d, w, row_max, row_sum);                 \
+    } while (0)
         if (h == 1) IGR_SM(1, IGR_SOFTMAX_R);
         else if (h == 2) IGR_SM(2, IGR_SOFTMAX_R);
         else if (h == 4 && vec) IGR_SM(4, IGR_SOFTMAX_R);
         else if (h == 8 && vec) IGR_SM(8, (IGR_SOFTMAX_R + 1) / 2);
-        else
+        else  // other head counts: every row by one wave
             hipLaunchKernelGGL(att_softmax_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0,
                                st, g->n_rows, h, g->row_ptr, g->edge_id, alpha, keep, sqrt_d, w, row_max,
                                row_sum);
@@ -685,15 +910,28 @@ extern "C" int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float 
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         const bool wide = wide_rows(g);
-        const dim3 g16((unsigned)((g->n_rows + 15) / 16)), g64((unsigned)((g->n_rows + 3) / 4));
+        const bool planned = split_plan(g);
+        const int64_t nr = planned ? g->n_order : g->n_rows;
+        const int32_t *order = planned ? g->order : nullptr;
+        const dim3 g16((unsigned)((nr + 15) / 16)), g64((unsigned)((nr + 3) / 4));
         const bool vec = (reinterpret_cast<uintptr_t>(alpha) & 15u) == 0;
 #define IGR_SMB(HH, RR)                                                                                           \
-    if (wide)                                                                                                     \
-        hipLaunchKernelGGL((att_softmax_bwd_g16_kernel<HH, RR, 64>), g64, dim3(256), 0, st, g->n_rows,           \
-                           g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha);            \
-    else                                                                                                          \
-        hipLaunchKernelGGL((att_softmax_bwd_g16_kernel<HH, RR, 16>), g16, dim3(256), 0, st, g->n_rows,           \
-                           g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha)
+    do {                                                                                                          \
+        if (nr > 0) {                                                                                             \
+            if (wide)                                                                                             \
+                hipLaunchKernelGGL((att_softmax_bwd_g16_kernel<HH, RR, 64>), g64, dim3(256), 0, st, nr,          \
+                                   g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha,     \
+                                   order);                                                                       \
+            else                                                                                                  \
+                hipLaunchKernelGGL((att_softmax_bwd_g16_kernel<HH, RR, 16>), g16, dim3(256), 0, st, nr,          \
+                                   g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha,     \
+                                   order);                                                                       \
+        }                                                                                                         \
+        if (planned)                                                                                              \
+            hipLaunchKernelGGL((att_softmax_bwd_block_kernel<HH, kSoftmaxBlock, kSoftmaxBlockR>),                 \
+                               dim3((unsigned)g->n_split), dim3(kSoftmaxBlock), 0, st, g->n_split, g->split_row,  \
+                               g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha);        \
+    } while (0)
         if (h == 1) IGR_SMB(1, IGR_SOFTMAX_R);
         else if (h == 2) IGR_SMB(2, IGR_SOFTMAX_R);
         else if (h == 4 && vec) IGR_SMB(4, IGR_SOFTMAX_R);

@@ -531,11 +531,30 @@ __global__ __launch_bounds__(256) void uniforms_kernel(int64_t n_rows, const int
                                                        const int64_t *__restrict__ eid, uint64_t seed, uint64_t offset,
                                                        const int64_t *__restrict__ offset_dev, int swap,
                                                        const float *__restrict__ val, float keep,
-                                                       float *__restrict__ out) {
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= n_rows) return;
+                                                       float *__restrict__ out, RowPlan plan, int planned) {
+    // planned: a wave takes one chunk of a split row or one whole unsplit row (a hub row
+    // is otherwise one wave's loop); else wave w takes row w
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    int64_t r, b, e;
+    if (planned) {
+        if (w >= plan.n_chunks + plan.n_order) return;
+        if (w < plan.n_chunks) {
+            r = plan.chunk_row[w];
+            b = plan.chunk_beg[w];
+            e = min(b + plan.chunk_edges, row_ptr[r + 1]);
+        } else {
+            r = plan.order[w - plan.n_chunks];
+            b = row_ptr[r];
+            e = row_ptr[r + 1];
+        }
+    } else {
+        r = w;
+        if (r >= n_rows) return;
+        b = row_ptr[r];
+        e = row_ptr[r + 1];
+    }
     const uint64_t off = offset + (offset_dev ? (uint64_t)*offset_dev : 0);
-    for (int64_t p = row_ptr[r] + (threadIdx.x & 63); p < row_ptr[r + 1]; p += 64) {
+    for (int64_t p = b + (threadIdx.x & 63); p < e; p += 64) {
         const uint32_t c = (uint32_t)col[p];
         const float u = uniform24(seed, off, swap ? edge_key(c, (uint32_t)r) : edge_key((uint32_t)r, c));
         if (!val) {
@@ -672,9 +691,11 @@ extern "C" int igr_dropout_uniforms(const igr_csr *g, uint64_t seed, uint64_t of
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         if (g->n_rows > 4294967295LL || g->n_cols > 4294967295LL)
             return arg_error("igr_dropout_uniforms", "dropout keys need row / column ids below 2^32");
-        hipLaunchKernelGGL(uniforms_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0, st, g->n_rows,
+        const bool planned = use_row_plan(g);
+        const int64_t waves = planned ? g->n_chunks + g->n_order : g->n_rows;
+        hipLaunchKernelGGL(uniforms_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, g->n_rows,
                            g->row_ptr, g->col_idx, g->edge_id, seed, offset, offset_dev, transposed ? 1 : 0,
-                           (const float *)nullptr, 1.f, out);
+                           (const float *)nullptr, 1.f, out, row_plan_of(g), planned ? 1 : 0);
         return launch_status("igr_dropout_uniforms");
     });
 }
@@ -689,9 +710,11 @@ extern "C" int igr_edge_dropout_counter_f32(const igr_csr *g, const float *val, 
         if (g->n_rows > 4294967295LL || g->n_cols > 4294967295LL)
             return arg_error(fn, "dropout keys need row / column ids below 2^32");
         const float keep = (float)(1.0 - (double)p);
-        hipLaunchKernelGGL(uniforms_kernel, dim3((unsigned)((g->n_rows + 3) / 4)), dim3(256), 0,
+        const bool planned = use_row_plan(g);
+        const int64_t waves = planned ? g->n_chunks + g->n_order : g->n_rows;
+        hipLaunchKernelGGL(uniforms_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                            reinterpret_cast<hipStream_t>(stream), g->n_rows, g->row_ptr, g->col_idx, g->edge_id, seed,
-                           offset, offset_dev, transposed ? 1 : 0, val, keep, out);
+                           offset, offset_dev, transposed ? 1 : 0, val, keep, out, row_plan_of(g), planned ? 1 : 0);
         return launch_status(fn);
     });
 }

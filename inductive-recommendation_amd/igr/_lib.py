@@ -85,6 +85,9 @@ SIGNATURES = {
     'igr_sddmm_dot_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     'igr_sddmm_shared_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     'igr_spmm_shared_heads_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    'igr_spmm_shared_heads_workspace_size': (c_i64, [_P(IgrCsr), c_i32, c_i32]),
+    'igr_spmm_shared_heads_ws_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
+                                                    c_i64, c_vp]),
     'igr_segment_reduce_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_i32, c_vp, c_vp]),
     'igr_att_softmax_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),
     'igr_att_softmax_bwd_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp,

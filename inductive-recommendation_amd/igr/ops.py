@@ -280,7 +280,7 @@ def sddmm_shared(g: Graph, u, v, h, out=None):
 
 
 def spmm_shared_heads(g: Graph, x, rhs, h, out=None):
-    """out[r, j*d:(j+1)*d] = sum_{p in row r} rhs[eid(p), j] * x[col_p, :] (igr_spmm_shared_heads_f32)."""
+    """out[r, j*d:(j+1)*d] = sum_{p in row r} rhs[eid(p), j] * x[col_p, :] (igr_spmm_shared_heads_ws_f32)."""
     _dev(x, rhs, out)
     x, ldx = _rows(x)
     d = x.shape[1]
@@ -289,8 +289,9 @@ def spmm_shared_heads(g: Graph, x, rhs, h, out=None):
         raise IgrError(f'spmm_shared_heads: x {tuple(x.shape)}, rhs {tuple(rhs.shape)} for {g.nnz} edges x {h} heads')
     if out is None:
         out = torch.empty(g.n_rows, h * d, dtype=torch.float32, device=x.device)
-    L.call('igr_spmm_shared_heads_f32', ctypes.byref(g.csr), h, d, _p(x), ldx, _p(rhs), _p(out), out.stride(0),
-           _stream())
+    ws = g.workspace(h * d)  # chunk partials of the split rows (None when no row is split)
+    L.call('igr_spmm_shared_heads_ws_f32', ctypes.byref(g.csr), h, d, _p(x), ldx, _p(rhs), _p(out), out.stride(0),
+           _p(ws), 0 if ws is None else ws.numel() * 4, _stream())
     return out
 
 

@@ -39,6 +39,9 @@ def main():
     ap.add_argument('--sharded', action='store_true',
                     help='igr.dist_train.ShardedIGCN (one rank per GPU under torch.distributed.run; '
                          'per-rank batch --batch)')
+    ap.add_argument('--skewed', default=None, metavar='SHAPE',
+                    help="MovieLens-like item popularity: the training pairs of tests/golden/ml_like.py's SHAPE "
+                         "('ml100k', 'ml1m', 'ml1m_l3', 'gowalla') instead of uniform draws (sets users / items / d / layers)")
     args = ap.parse_args()
     from igr import model as M
     from igr import trainer as T
@@ -62,7 +65,15 @@ def main():
         while not building.wait(30):
             print(f'... setting up ({time.time() - t_hb:.0f}s)', file=sys.stderr, flush=True)
     threading.Thread(target=heartbeat, daemon=True).start()
-    pairs = synthetic_pairs(args.n_users, args.n_items, args.n_edges, 0)
+    if args.skewed:
+        sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
+        import ml_like
+        args.n_users, args.n_items, mean_deg, args.d, args.layers, _ = ml_like.SHAPES[args.skewed]
+        train, _, _ = ml_like.make_splits(args.n_users, args.n_items, mean_deg, seed=100)
+        pairs = np.array([[u, i] for u in range(args.n_users) for i in train[u]], dtype=np.int64)
+        args.n_edges = len(pairs)
+    else:
+        pairs = synthetic_pairs(args.n_users, args.n_items, args.n_edges, 0)
 
     class DS:
         name = 'synthetic'

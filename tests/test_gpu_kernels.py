@@ -1089,3 +1089,46 @@ def test_edge_dropout_counter_equals_two_step_form(dedup):
             got = ops.edge_dropout_counter(g, val, 0.3, 1234, 5, swap=swap, offset_dev=ctr)
             assert torch.equal(got, ref)
             assert 0.2 < float((got == 0).float().mean()) < 0.4
+
+
+@pytest.mark.parametrize('dedup', [True, False])
+def test_attention_kernels_split_rows_against_whole_rows(dedup):
+    """The attention edge kernels take a graph's schedule: the chunks of split rows and the
+    unsplit rows (SDDMM, dropout draws), chunk partials + an ordered combine (the SDDMM's
+    gradient), lane groups for unsplit rows + a workgroup per split row (edge softmax and
+    its backward).  Same graph under a plan that splits most rows and under one that
+    splits none: per-edge results bit for bit, reductions within fp32 reassociation."""
+    base, _ = rand_graph(400, 6000, 30000, seed=77, skew=True, dedup=dedup)
+    hst = base.host()
+    mk = lambda T, C: G.Graph(hst['row_ptr'], hst['col_idx'], 400, 6000, device=DEV, edge_id=hst['edge_id'],  # noqa: E731
+                              split_threshold=T, chunk_edges=C)
+    cut, whole = mk(32, 64), mk(1 << 30, 1 << 30)
+    assert cut.n_split > 50 and cut.n_chunks > cut.n_split and whole.n_split == 0
+    assert int(np.diff(hst['row_ptr']).max()) > 2048  # a hub row longer than a workgroup's register cache
+    h, d = 4, 64
+    rng = np.random.default_rng(5)
+    u = t(rng.standard_normal((400, h * d)).astype(np.float32))
+    v = t(rng.standard_normal((6000, d)).astype(np.float32))
+    rhs = t(rng.standard_normal((base.nnz, h)).astype(np.float32))
+    assert torch.equal(ops.sddmm_shared(cut, u, v, h), ops.sddmm_shared(whole, u, v, h))
+    assert torch.equal(ops.sddmm_shared(cut, u[:, :d].contiguous(), v, 1), ops.sddmm_shared(whole, u[:, :d].contiguous(), v, 1))
+    y_cut, y_whole = ops.spmm_shared_heads(cut, v, rhs, h), ops.spmm_shared_heads(whole, v, rhs, h)
+    close(y_cut.cpu().numpy(), y_whole.cpu().numpy(), rtol=1e-5, atol_row=2e-6)
+    assert torch.equal(y_cut, ops.spmm_shared_heads(cut, v, rhs, h))  # ordered combine: same bits again
+    val = t(rng.standard_normal(base.nnz).astype(np.float32))
+    for swap in (False, True):
+        assert torch.equal(ops.edge_dropout_counter(cut, val, 0.3, 99, 3, swap=swap),
+                           ops.edge_dropout_counter(whole, val, 0.3, 99, 3, swap=swap))
+    sd = ops.sqrt_scale(d)
+    keep = t((rng.random(base.nnz) > 0.3).astype(np.float32))
+    dw = t(rng.standard_normal(base.nnz).astype(np.float32))
+    for kp in (None, keep):
+        res = []
+        for g in (cut, whole):
+            a = (rhs * 30).clone().requires_grad_(True)
+            w = ops.AttSoftmax.apply(g, a, sd, kp)
+            w.backward(dw)
+            res.append((w.detach().cpu().numpy(), a.grad.cpu().numpy()))
+        close(res[0][0], res[1][0], rtol=2e-5, atol_row=1e-6)
+        gr, g0 = res[0][1].astype(np.float64), res[1][1].astype(np.float64)
+        assert np.all(np.abs(gr - g0) <= 1e-4 * np.abs(g0) + 1e-5 * np.abs(g0).max())

@@ -409,6 +409,37 @@ __global__ __launch_bounds__(NT) void spmm_combine(const int32_t *__restrict__ s
     if (slot == 0) store_row4(epi, split_row[i], sub * 4, red[0][sub]);
 }
 
+// The same for graphs whose split rows have few chunks each (a small graph with a low
+// split threshold: thousands of split rows of 2-3 chunks): a wave per split row, four rows
+// per workgroup, no LDS and no barrier.  The wave's 64 / (D / 4) slots take alternate
+// chunks and are added in a fixed xor tree.
+template <int D>
+__global__ __launch_bounds__(256) void spmm_combine_wave(const int32_t *__restrict__ split_row,
+                                                         const int64_t *__restrict__ split_ptr,
+                                                         int64_t n_split, const float *__restrict__ ws, Epi epi) {
+    constexpr int LPR = D / 4;
+    constexpr int S = 64 / LPR;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n_split) return;
+    const int lane = threadIdx.x & 63;
+    const int slot = lane / LPR;
+    const int sub = lane - slot * LPR;
+    const int32_t r = split_row[i];
+    if (epi.row_mask && !bit_set(epi.row_mask, r)) return;  // wave-uniform
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t e = split_ptr[i + 1];
+    for (int64_t c = split_ptr[i] + slot; c < e; c += S)
+        a = f4_add(a, *reinterpret_cast<const float4 *>(ws + c * D + sub * 4));
+#pragma unroll
+    for (int m = LPR; m < 64; m <<= 1) {
+        a.x += shfl_xor_f(a.x, m);
+        a.y += shfl_xor_f(a.y, m);
+        a.z += shfl_xor_f(a.z, m);
+        a.w += shfl_xor_f(a.w, m);
+    }
+    if (slot == 0) store_row4(epi, r, sub * 4, a);
+}
+
 // Any d / alignment: one wave per row, lanes over features.
 template <class W>
 __global__ __launch_bounds__(256) void spmm_generic(int64_t n_rows, int d,
@@ -455,6 +486,9 @@ static void launch_fast(const igr_csr *g, const float *x, int64_t ldx, const W &
         if (g->n_chunks >= 64 * g->n_split)
             hipLaunchKernelGGL((spmm_combine<D, 1024>), dim3((unsigned)g->n_split), dim3(1024), 0, st, g->split_row,
                                g->split_ptr, g->n_split, ws, epi);
+        else if (g->n_chunks <= 8 * g->n_split)
+            hipLaunchKernelGGL((spmm_combine_wave<D>), dim3((unsigned)((g->n_split + 3) / 4)), dim3(256), 0, st,
+                               g->split_row, g->split_ptr, g->n_split, ws, epi);
         else
             hipLaunchKernelGGL((spmm_combine<D, 256>), dim3((unsigned)g->n_split), dim3(256), 0, st, g->split_row,
                                g->split_ptr, g->n_split, ws, epi);

@@ -39,6 +39,8 @@ def main():
     ap.add_argument('--sharded', action='store_true',
                     help='igr.dist_train.ShardedIGCN (one rank per GPU under torch.distributed.run; '
                          'per-rank batch --batch)')
+    ap.add_argument('--item-dist', default='uniform', choices=['uniform', 'zipf'],
+                    help='item popularity of the synthetic draws (zipf: exponent 1.1)')
     ap.add_argument('--skewed', default=None, metavar='SHAPE',
                     help="MovieLens-like item popularity: the training pairs of tests/golden/ml_like.py's SHAPE "
                          "('ml100k', 'ml1m', 'ml1m_l3', 'gowalla') instead of uniform draws (sets users / items / d / layers)")
@@ -73,7 +75,7 @@ def main():
         pairs = np.array([[u, i] for u in range(args.n_users) for i in train[u]], dtype=np.int64)
         args.n_edges = len(pairs)
     else:
-        pairs = synthetic_pairs(args.n_users, args.n_items, args.n_edges, 0)
+        pairs = synthetic_pairs(args.n_users, args.n_items, args.n_edges, 0, args.item_dist)
 
     class DS:
         name = 'synthetic'

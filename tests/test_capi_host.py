@@ -227,3 +227,45 @@ def test_new_entry_points_validate_arguments():
     _refused('igr_adam_f32', 4, F, F, F, F, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None, st, match='step')
     _refused('igr_bpr_sample', 4, 0, F, F, F, 10, 1, 0, None, 8, F, F, F, st, match='active')
     _refused('igr_spmm_heads_f32', ctypes.byref(rect.csr), 4, 64, F, 64, F, F, 256, None, st, match='leading')
+
+
+def test_shared_heads_workspace_contract():
+    """igr_spmm_shared_heads_ws_f32: the workspace holds one h * d partial per chunk of the
+    graph's split rows (none when no row is split); a smaller or misaligned one is refused."""
+    F = ctypes.c_void_p(0x10000)
+    rp = np.array([0, 700, 705, 2000], np.int64)
+    ci = np.zeros(2000, np.int32)
+    cut = G.Graph(rp, ci, 3, 8, device='cpu', split_threshold=128, chunk_edges=256)
+    whole = G.Graph(rp, ci, 3, 8, device='cpu', split_threshold=1 << 30, chunk_edges=1 << 30)
+    assert (cut.n_split, cut.n_chunks, whole.n_chunks) == (2, 3 + 6, 0)
+    size = _lib.lib().igr_spmm_shared_heads_workspace_size
+    assert size(ctypes.byref(cut.csr), 4, 64) == 9 * 4 * 64 * 4
+    assert size(ctypes.byref(whole.csr), 4, 64) == 0 and size(None, 4, 64) == 0
+    _refused('igr_spmm_shared_heads_ws_f32', ctypes.byref(cut.csr), 4, 64, F, 64, F, F, 256, F, 9 * 4 * 64 * 4 - 1, None,
+             match='workspace smaller')
+    _refused('igr_spmm_shared_heads_ws_f32', ctypes.byref(cut.csr), 4, 64, F, 64, F, F, 256, ctypes.c_void_p(0x10004),
+             9 * 4 * 64 * 4, None, match='16-byte')
+    _refused('igr_spmm_shared_heads_ws_f32', ctypes.byref(cut.csr), 3, 64, F, 64, F, F, 256, F, 1 << 20, None,
+             match='supported')
+
+
+def test_auto_plan_is_a_function_of_the_degrees():
+    """igr.graph.auto_plan: the default plan for graphs of alike rows and for graphs above
+    4 M edges; a lower split threshold when a few rows are far longer than the rest; the
+    same answer for the same degrees (runs stay bitwise reproducible)."""
+    rng = np.random.default_rng(0)
+    alike = np.concatenate([[0], np.cumsum(rng.integers(150, 330, 9746))])
+    assert G.auto_plan(alike) == (512, 512)
+    deg = rng.integers(20, 200, 9746)
+    deg[:300] = rng.integers(600, 4000, 300)  # hub rows
+    skew = np.concatenate([[0], np.cumsum(deg)])
+    t, c = G.auto_plan(skew)
+    assert t < 512 and c == min(2 * t, 512) and G.auto_plan(skew.copy()) == (t, c)
+    big = np.concatenate([[0], np.cumsum(np.full(30000, 200))])  # 6 M edges
+    assert G.auto_plan(big) == (512, 512)
+    short = np.concatenate([[0], np.cumsum(rng.integers(0, 60, 5000))])  # nothing to split
+    assert G.auto_plan(short) == (512, 512)
+    g = G.Graph(skew, np.zeros(int(skew[-1]), np.int32), len(deg), 1, device='cpu')
+    assert (g.split_threshold, g.chunk_edges) == (t, c) and g.n_split > 0
+    assert G.Graph(skew, np.zeros(int(skew[-1]), np.int32), len(deg), 1, device='cpu', split_threshold=512,
+                   chunk_edges=512).split_threshold == 512

@@ -343,6 +343,18 @@ int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alpha, const f
 int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float *alpha, const float *keep,
                             float sqrt_d, const float *row_max, const float *row_sum, const float *dw,
                             float *dalpha, void *stream);
+/* The two with a workspace (igr_att_softmax_workspace_size bytes; the backward uses half):
+ * the rows the graph's schedule splits are then processed chunk by chunk, a wave per chunk
+ * (per-chunk max and sum, a per-row combine in chunk order, per-chunk weights), so a hub
+ * row of any length is spread over the chip; row_max and row_sum must be given.  NULL
+ * workspace = a workgroup per split row, as the plain entry points.  Deterministic. */
+int64_t igr_att_softmax_workspace_size(const igr_csr *g, int32_t h);
+int igr_att_softmax_ws_f32(const igr_csr *g, int32_t h, const float *alpha, const float *keep, float sqrt_d,
+                           float *w, float *row_max, float *row_sum, float *workspace, int64_t workspace_bytes,
+                           void *stream);
+int igr_att_softmax_bwd_ws_f32(const igr_csr *g, int32_t h, const float *alpha, const float *keep, float sqrt_d,
+                               const float *row_max, const float *row_sum, const float *dw, float *dalpha,
+                               float *workspace, int64_t workspace_bytes, void *stream);
 
 /* NGCF.dropout_sp_mat (model.py:4016-4028) as a value mask over the fixed
  * CSR: out = floor((1-p) + rand) ? val / (1-p) : 0.  rand ~ U[0,1), [n]. */

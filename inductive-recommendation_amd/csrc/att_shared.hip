@@ -278,24 +278,41 @@ __global__ __launch_bounds__(256) void spmm_shared_heads_kernel(int64_t n_rows, 
     }
 }
 
-// y[split_row[s], :] = the sum of the row's chunk partials, in chunk order (one block per
-// split row, one float4 column group per thread; width = H * D floats <= 512).
-__global__ __launch_bounds__(128) void heads_combine_kernel(int64_t n_split, const int32_t *__restrict__ split_row,
+// y[split_row[s], :] = the sum of the row's chunk partials (one block per split row;
+// width = H * D floats <= 512, one float4 column group per thread).  The block's
+// 256 / (width / 4) slots take alternate chunks - a hub row has thousands - and are
+// added in slot order through LDS: a fixed order, the same bits on every run.
+__global__ __launch_bounds__(256) void heads_combine_kernel(int64_t n_split, const int32_t *__restrict__ split_row,
                                                             const int64_t *__restrict__ split_ptr,
                                                             const float *__restrict__ ws, int width,
                                                             float *__restrict__ y, int64_t ldy) {
+    __shared__ float4 red[256];
     const int64_t s = blockIdx.x;
-    const int t = threadIdx.x * 4;
-    if (s >= n_split || t >= width) return;
+    const int cols = width / 4;          // 8 ... 128, a power of two
+    const int slots = 256 / cols;
+    const int slot = threadIdx.x / cols;
+    const int t = threadIdx.x - slot * cols;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t k = split_ptr[s]; k < split_ptr[s + 1]; ++k) {
-        const float4 p = *reinterpret_cast<const float4 *>(ws + k * width + t);
+    if (s < n_split) {
+        for (int64_t k = split_ptr[s] + slot; k < split_ptr[s + 1]; k += slots) {
+            const float4 p = *reinterpret_cast<const float4 *>(ws + k * width + t * 4);
+            acc.x += p.x;
+            acc.y += p.y;
+            acc.z += p.z;
+            acc.w += p.w;
+        }
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (s >= n_split || slot != 0) return;
+    for (int k = 1; k < slots; ++k) {
+        const float4 p = red[k * cols + t];
         acc.x += p.x;
         acc.y += p.y;
         acc.z += p.z;
         acc.w += p.w;
     }
-    *reinterpret_cast<float4 *>(y + (int64_t)split_row[s] * ldy + t) = acc;
+    *reinterpret_cast<float4 *>(y + (int64_t)split_row[s] * ldy + t * 4) = acc;
 }
 
 template <template <int, int> class Launch, class... Args>
@@ -344,7 +361,7 @@ struct LaunchSpmmShared {
             hipLaunchKernelGGL((spmm_shared_heads_kernel<D, H, true>), grid, dim3(256), 0, st, g->n_rows, g->row_ptr,
                                g->col_idx, g->edge_id, plan, x, (int)ldx, rhs, y, ldy, ws);
             if (g->n_split > 0)
-                hipLaunchKernelGGL(heads_combine_kernel, dim3((unsigned)g->n_split), dim3(128), 0, st, g->n_split,
+                hipLaunchKernelGGL(heads_combine_kernel, dim3((unsigned)g->n_split), dim3(256), 0, st, g->n_split,
                                    g->split_row, g->split_ptr, ws, H * D, y, ldy);
         } else {
             hipLaunchKernelGGL((spmm_shared_heads_kernel<D, H, false>), grid, dim3(256), 0, st, g->n_rows, g->row_ptr,

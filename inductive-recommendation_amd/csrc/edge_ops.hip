@@ -670,6 +670,218 @@ __global__ __launch_bounds__(NT) void att_softmax_bwd_block_kernel(
     }
 }
 
+// ---------------------------------------------------------------- split rows by chunks (with a workspace)
+// With a workspace the split rows go chunk by chunk instead, a wave per chunk of the
+// schedule, so a row of any length is spread over the chip (a workgroup per row walks a
+// 2 M-edge hub row for milliseconds).  Forward: (1) per chunk the max m_c and
+// s_c = sum exp((a - m_c) / t) per head; (2) per split row m = max_c m_c and
+// s = sum_c s_c exp((m_c - m) / t), the chunks in order across the lanes and a fixed xor
+// tree (t = sqrt_d * 10, the temperature of att_exp); (3) per chunk the weights.  Backward:
+// per-chunk sums of a * g, their per-row totals written back over every chunk slot of the
+// row, then per chunk the gradient.  Slots: 2 H floats per chunk forward, H backward.
+template <int H>
+__global__ __launch_bounds__(256) void att_softmax_chunk_stats_kernel(
+    RowPlan plan, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
+    const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d, float *__restrict__ ws) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= plan.n_chunks) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = plan.chunk_beg[c], e = min(b + plan.chunk_edges, row_ptr[plan.chunk_row[c] + 1]);
+    float m[H], sm[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) m[j] = -INFINITY;
+    for (int64_t p = b + lane; p < e; p += 64) {
+        const int64_t ee = eid ? eid[p] : p;
+        if (!kept(keep, ee)) continue;
+        float x[H];
+        load_heads<H>(alpha, ee, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) m[j] = fmaxf(m[j], x[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        m[j] = gmax<64>(m[j]);
+        sm[j] = 0.f;
+    }
+    for (int64_t p = b + lane; p < e; p += 64) {
+        const int64_t ee = eid ? eid[p] : p;
+        if (!kept(keep, ee)) continue;
+        float x[H];
+        load_heads<H>(alpha, ee, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) sm[j] += att_exp(x[j], m[j], sqrt_d);
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) sm[j] = gsum<64>(sm[j]);
+    if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            ws[c * (2 * H) + j] = m[j];
+            ws[c * (2 * H) + H + j] = sm[j];
+        }
+    }
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void att_softmax_row_stats_kernel(
+    int64_t n_split, const int32_t *__restrict__ split_row, const int64_t *__restrict__ split_ptr,
+    const float *__restrict__ ws, float sqrt_d, float *__restrict__ row_max, float *__restrict__ row_sum) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n_split) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = split_ptr[i], e = split_ptr[i + 1];
+    float m[H], sm[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) m[j] = -INFINITY;
+    for (int64_t c = b + lane; c < e; c += 64) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) m[j] = fmaxf(m[j], ws[c * (2 * H) + j]);
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        m[j] = gmax<64>(m[j]);
+        sm[j] = 0.f;
+    }
+    for (int64_t c = b + lane; c < e; c += 64) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            const float mc = ws[c * (2 * H) + j];
+            if (mc != -INFINITY) sm[j] += ws[c * (2 * H) + H + j] * att_exp(mc, m[j], sqrt_d);  // a chunk with no kept edge adds nothing
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) sm[j] = gsum<64>(sm[j]);
+    if (lane == 0) {
+        const int64_t r = split_row[i];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            row_max[r * H + j] = m[j];
+            row_sum[r * H + j] = sm[j];
+        }
+    }
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void att_softmax_chunk_write_kernel(
+    RowPlan plan, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
+    const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d,
+    const float *__restrict__ row_max, const float *__restrict__ row_sum, float *__restrict__ w) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= plan.n_chunks) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = plan.chunk_row[c];
+    const int64_t b = plan.chunk_beg[c], e = min(b + plan.chunk_edges, row_ptr[r + 1]);
+    float m[H], sm[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        m[j] = row_max[r * H + j];
+        sm[j] = row_sum[r * H + j];
+    }
+    for (int64_t p = b + lane; p < e; p += 64) {
+        const int64_t ee = eid ? eid[p] : p;
+        if (!kept(keep, ee)) {
+            w[ee] = 0.f;
+            continue;
+        }
+        float x[H];
+        load_heads<H>(alpha, ee, x);
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < H; ++j) acc += att_exp(x[j], m[j], sqrt_d) / sm[j];
+        w[ee] = acc / (float)H;
+    }
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void att_softmax_bwd_chunk_sums_kernel(
+    RowPlan plan, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
+    const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d,
+    const float *__restrict__ row_max, const float *__restrict__ row_sum, const float *__restrict__ dw,
+    float *__restrict__ ws) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= plan.n_chunks) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = plan.chunk_row[c];
+    const int64_t b = plan.chunk_beg[c], e = min(b + plan.chunk_edges, row_ptr[r + 1]);
+    float m[H], s[H], S[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        m[j] = row_max[r * H + j];
+        s[j] = row_sum[r * H + j];
+        S[j] = 0.f;
+    }
+    const float inv_h = 1.f / (float)H;
+    for (int64_t p = b + lane; p < e; p += 64) {
+        const int64_t ee = eid ? eid[p] : p;
+        if (!kept(keep, ee)) continue;
+        const float gg = dw[ee] * inv_h;
+        float x[H];
+        load_heads<H>(alpha, ee, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) S[j] += att_exp(x[j], m[j], sqrt_d) / s[j] * gg;
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) S[j] = gsum<64>(S[j]);
+    if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) ws[c * H + j] = S[j];
+    }
+}
+
+// ws[c, :] <- the sum over the row's chunks of ws[c', :], for every chunk c of the row
+template <int H>
+__global__ __launch_bounds__(256) void att_softmax_bwd_row_sums_kernel(int64_t n_split,
+                                                                       const int64_t *__restrict__ split_ptr,
+                                                                       float *__restrict__ ws) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n_split) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = split_ptr[i], e = split_ptr[i + 1];
+    float S[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) S[j] = 0.f;
+    for (int64_t c = b + lane; c < e; c += 64) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) S[j] += ws[c * H + j];
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) S[j] = gsum<64>(S[j]);  // every lane holds the total before any slot is overwritten
+    for (int64_t c = b + lane; c < e; c += 64) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) ws[c * H + j] = S[j];
+    }
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void att_softmax_bwd_chunk_write_kernel(
+    RowPlan plan, const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ eid,
+    const float *__restrict__ alpha, const float *__restrict__ keep, float sqrt_d,
+    const float *__restrict__ row_max, const float *__restrict__ row_sum, const float *__restrict__ dw,
+    const float *__restrict__ ws, float *__restrict__ dalpha) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= plan.n_chunks) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = plan.chunk_row[c];
+    const int64_t b = plan.chunk_beg[c], e = min(b + plan.chunk_edges, row_ptr[r + 1]);
+    float m[H], s[H], S[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        m[j] = row_max[r * H + j];
+        s[j] = row_sum[r * H + j];
+        S[j] = ws[c * H + j];
+    }
+    const float inv_h = 1.f / (float)H, cc = sqrt_d * 10.f;
+    for (int64_t p = b + lane; p < e; p += 64) {
+        const int64_t ee = eid ? eid[p] : p;
+        const bool kk = kept(keep, ee);
+        const float gg = dw[ee] * inv_h;
+        float x[H];
+        if (kk) load_heads<H>(alpha, ee, x);
+#pragma unroll
+        for (int j = 0; j < H; ++j) dalpha[ee * H + j] = kk ? att_exp(x[j], m[j], sqrt_d) / s[j] * (gg - S[j]) / cc : 0.f;
+    }
+}
+
 // gspmm copy_rhs sum / max with 16 lanes per row and all H heads per lane
 // (the segment_reduce_kernel above takes a wave per row and a pass per head).
 template <int H, int LPR>
@@ -859,9 +1071,25 @@ extern "C" int igr_segment_reduce_f32(const igr_csr *g, int32_t h, const float *
 
 extern "C" int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alpha, const float *keep,
                                    float sqrt_d, float *w, float *row_max, float *row_sum, void *stream) {
-    return guarded("igr_att_softmax_f32", [&]() -> int {
-        const char *fn = "igr_att_softmax_f32";
+    return igr_att_softmax_ws_f32(g, h, alpha, keep, sqrt_d, w, row_max, row_sum, nullptr, 0, stream);
+}
+
+extern "C" int64_t igr_att_softmax_workspace_size(const igr_csr *g, int32_t h) {
+    if (!g || h <= 0 || g->n_chunks <= 0) return 0;
+    return g->n_chunks * (int64_t)(2 * h) * (int64_t)sizeof(float);
+}
+
+extern "C" int igr_att_softmax_ws_f32(const igr_csr *g, int32_t h, const float *alpha, const float *keep,
+                                      float sqrt_d, float *w, float *row_max, float *row_sum, float *workspace,
+                                      int64_t workspace_bytes, void *stream) {
+    return guarded("igr_att_softmax_ws_f32", [&]() -> int {
+        const char *fn = "igr_att_softmax_ws_f32";
         if (!g || h <= 0 || h > kMaxHeads) return arg_error(fn, "h must be in [1, 8]");
+        if (workspace && workspace_bytes < igr_att_softmax_workspace_size(g, h))
+            return arg_error(fn, "workspace smaller than igr_att_softmax_workspace_size");
+        // the chunked path hands the row max / sum from its second launch to its third
+        const bool chunked = workspace != nullptr && row_max != nullptr && row_sum != nullptr && has_row_plan(g) &&
+                             g->n_chunks > 0 && g->split_ptr != nullptr;
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         const bool wide = wide_rows(g);
@@ -882,7 +1110,15 @@ extern "C" int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alp
                 hipLaunchKernelGGL((att_softmax_g16_kernel<HH, RR, 16>), g16, dim3(256), 0, st, nr, g->row_ptr,  \
                                    g->edge_id, alpha, keep, sqrt_d, w, row_max, row_sum, order);                 \
         }                                                                                                         \
-        if (planned)                                                                                              \
+        if (planned && chunked) {                                                                                 \
+            const dim3 gc((unsigned)((g->n_chunks + 3) / 4)), gs((unsigned)((g->n_split + 3) / 4));               \
+            hipLaunchKernelGGL((att_softmax_chunk_stats_kernel<HH>), gc, dim3(256), 0, st, row_plan_of(g),        \
+                               g->row_ptr, g->edge_id, alpha, keep, sqrt_d, workspace);                           \
+            hipLaunchKernelGGL((att_softmax_row_stats_kernel<HH>), gs, dim3(256), 0, st, g->n_split,              \
+                               g->split_row, g->split_ptr, workspace, sqrt_d, row_max, row_sum);                  \
+            hipLaunchKernelGGL((att_softmax_chunk_write_kernel<HH>), gc, dim3(256), 0, st, row_plan_of(g),        \
+                               g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, w);                 \
+        } else if (planned)                                                                                       \
             hipLaunchKernelGGL((att_softmax_block_kernel<HH, kSoftmaxBlock, kSoftmaxBlockR>),                     \
                                dim3((unsigned)g->n_split), dim3(kSoftmaxBlock), 0, st, g->n_split, g->split_row,  \
                                g->row_ptr, g->edge_id, alpha, keep, sqrt_d, w, row_max, row_sum);                 \
@@ -903,10 +1139,19 @@ extern "C" int igr_att_softmax_f32(const igr_csr *g, int32_t h, const float *alp
 extern "C" int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float *alpha,
                                        const float *keep, float sqrt_d, const float *row_max,
                                        const float *row_sum, const float *dw, float *dalpha, void *stream) {
-    return guarded("igr_att_softmax_bwd_f32", [&]() -> int {
-        const char *fn = "igr_att_softmax_bwd_f32";
+    return igr_att_softmax_bwd_ws_f32(g, h, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha, nullptr, 0, stream);
+}
+
+extern "C" int igr_att_softmax_bwd_ws_f32(const igr_csr *g, int32_t h, const float *alpha, const float *keep,
+                                          float sqrt_d, const float *row_max, const float *row_sum, const float *dw,
+                                          float *dalpha, float *workspace, int64_t workspace_bytes, void *stream) {
+    return guarded("igr_att_softmax_bwd_ws_f32", [&]() -> int {
+        const char *fn = "igr_att_softmax_bwd_ws_f32";
         if (!g || h <= 0 || h > kMaxHeads) return arg_error(fn, "h must be in [1, 8]");
         if (!row_max || !row_sum) return arg_error(fn, "row_max / row_sum required");
+        if (workspace && workspace_bytes < igr_att_softmax_workspace_size(g, h) / 2)
+            return arg_error(fn, "workspace smaller than half of igr_att_softmax_workspace_size");
+        const bool chunked = workspace != nullptr && has_row_plan(g) && g->n_chunks > 0 && g->split_ptr != nullptr;
         if (g->n_rows == 0) return IGR_OK;
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         const bool wide = wide_rows(g);
@@ -927,7 +1172,16 @@ extern "C" int igr_att_softmax_bwd_f32(const igr_csr *g, int32_t h, const float 
                                    g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha,     \
                                    order);                                                                       \
         }                                                                                                         \
-        if (planned)                                                                                              \
+        if (planned && chunked) {                                                                                 \
+            const dim3 gc((unsigned)((g->n_chunks + 3) / 4)), gs((unsigned)((g->n_split + 3) / 4));               \
+            hipLaunchKernelGGL((att_softmax_bwd_chunk_sums_kernel<HH>), gc, dim3(256), 0, st, row_plan_of(g),     \
+                               g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, workspace);     \
+            hipLaunchKernelGGL((att_softmax_bwd_row_sums_kernel<HH>), gs, dim3(256), 0, st, g->n_split,           \
+                               g->split_ptr, workspace);                                                          \
+            hipLaunchKernelGGL((att_softmax_bwd_chunk_write_kernel<HH>), gc, dim3(256), 0, st, row_plan_of(g),    \
+                               g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, workspace,      \
+                               dalpha);                                                                           \
+        } else if (planned)                                                                                       \
             hipLaunchKernelGGL((att_softmax_bwd_block_kernel<HH, kSoftmaxBlock, kSoftmaxBlockR>),                 \
                                dim3((unsigned)g->n_split), dim3(kSoftmaxBlock), 0, st, g->n_split, g->split_row,  \
                                g->row_ptr, g->edge_id, alpha, keep, sqrt_d, row_max, row_sum, dw, dalpha);        \

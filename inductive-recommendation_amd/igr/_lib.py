@@ -92,6 +92,11 @@ SIGNATURES = {
     'igr_att_softmax_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),
     'igr_att_softmax_bwd_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp,
                                                c_vp]),
+    'igr_att_softmax_workspace_size': (c_i64, [_P(IgrCsr), c_i32]),
+    'igr_att_softmax_ws_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                              c_vp]),
+    'igr_att_softmax_bwd_ws_f32': (ctypes.c_int, [_P(IgrCsr), c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp,
+                                                  c_vp, c_i64, c_vp]),
     'igr_edge_dropout_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_f32, c_vp, c_vp]),
     'igr_feat_values_f32': (ctypes.c_int, [c_i64, c_vp, c_vp, c_f32, c_vp, c_vp]),
     'igr_gather_rows_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),

@@ -161,6 +161,7 @@ class Graph:
         assert len(row_ptr) == self.n_rows + 1, 'row_ptr must have n_rows + 1 entries'
         self.nnz = int(row_ptr[-1])
         assert len(col_idx) == self.nnz
+        self.max_row_edges = int(np.diff(row_ptr).max()) if self.n_rows else 0
         if edge_id is not None:
             edge_id = _np(edge_id, np.int64)
             if np.array_equal(edge_id, np.arange(self.nnz, dtype=np.int64)):

@@ -247,6 +247,15 @@ def test_shared_heads_workspace_contract():
              9 * 4 * 64 * 4, None, match='16-byte')
     _refused('igr_spmm_shared_heads_ws_f32', ctypes.byref(cut.csr), 3, 64, F, 64, F, F, 256, F, 1 << 20, None,
              match='supported')
+    # the edge softmax by chunks: 2 h floats per chunk forward, h backward
+    ssize = _lib.lib().igr_att_softmax_workspace_size
+    assert ssize(ctypes.byref(cut.csr), 4) == 9 * 8 * 4 and ssize(ctypes.byref(whole.csr), 4) == 0
+    _refused('igr_att_softmax_ws_f32', ctypes.byref(cut.csr), 4, F, None, 8.0, F, F, F, F, 9 * 8 * 4 - 1, None,
+             match='workspace smaller')
+    _refused('igr_att_softmax_bwd_ws_f32', ctypes.byref(cut.csr), 4, F, None, 8.0, F, F, F, F, F, 9 * 4 * 4 - 1, None,
+             match='workspace smaller')
+    _refused('igr_att_softmax_bwd_ws_f32', ctypes.byref(cut.csr), 4, F, None, 8.0, None, F, F, F, F, 1 << 20, None,
+             match='row_max')
 
 
 def test_auto_plan_is_a_function_of_the_degrees():

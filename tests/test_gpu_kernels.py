@@ -1126,9 +1126,23 @@ def test_attention_kernels_split_rows_against_whole_rows(dedup):
         res = []
         for g in (cut, whole):
             a = (rhs * 30).clone().requires_grad_(True)
+            g.max_row_edges = 1 << 30  # the chunked path whatever the row lengths (the default takes it above 8192 edges)
             w = ops.AttSoftmax.apply(g, a, sd, kp)
             w.backward(dw)
             res.append((w.detach().cpu().numpy(), a.grad.cpu().numpy()))
         close(res[0][0], res[1][0], rtol=2e-5, atol_row=1e-6)
         gr, g0 = res[0][1].astype(np.float64), res[1][1].astype(np.float64)
+        assert np.all(np.abs(gr - g0) <= 1e-4 * np.abs(g0) + 1e-5 * np.abs(g0).max())
+        # the plain entry points (no workspace): a workgroup per split row
+        import ctypes
+        from igr import _lib as L
+        a = (rhs * 30).contiguous()
+        P = lambda x: None if x is None else ctypes.c_void_p(x.data_ptr())  # noqa: E731
+        w2, rmax, rsum = torch.empty(base.nnz, device=DEV), torch.empty(400, h, device=DEV), torch.empty(400, h, device=DEV)
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        L.call('igr_att_softmax_f32', ctypes.byref(cut.csr), h, P(a), P(kp), float(sd), P(w2), P(rmax), P(rsum), st)
+        close(w2.cpu().numpy(), res[1][0], rtol=2e-5, atol_row=1e-6)
+        da = torch.empty_like(a)
+        L.call('igr_att_softmax_bwd_f32', ctypes.byref(cut.csr), h, P(a), P(kp), float(sd), P(rmax), P(rsum), P(dw), P(da), st)
+        gr = da.cpu().numpy().astype(np.float64)
         assert np.all(np.abs(gr - g0) <= 1e-4 * np.abs(g0) + 1e-5 * np.abs(g0).max())

@@ -922,8 +922,7 @@ __global__ void edge_dropout_kernel(int64_t n, const float *__restrict__ val,
     }
 }
 
-__global__ void feat_values_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr,
-                                   const float *__restrict__ row_sum, float ex,
+__global__ void feat_values_kernel(int64_t n_rows, const float *__restrict__ row_sum, float ex,
                                    float *__restrict__ out) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_rows;
          r += (int64_t)gridDim.x * blockDim.x) {
@@ -1234,8 +1233,8 @@ extern "C" int igr_feat_values_f32(int64_t n_rows, const int64_t *row_ptr, const
             hipLaunchKernelGGL(feat_values_edges_kernel, dim3(grid_for(n_rows * 16, 256)), dim3(256), 0, st, n_rows,
                                row_ptr, row_sum, exponent, out);
         else
-            hipLaunchKernelGGL(feat_values_kernel, dim3(grid_for(n_rows, 256)), dim3(256), 0, st, n_rows, row_ptr,
-                               row_sum, exponent, out);
+            hipLaunchKernelGGL(feat_values_kernel, dim3(grid_for(n_rows, 256)), dim3(256), 0, st, n_rows, row_sum,
+                               exponent, out);
         return launch_status("igr_feat_values_f32");
     });
 }

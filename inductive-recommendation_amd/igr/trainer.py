@@ -85,6 +85,43 @@ def calculate_metrics(eval_data, rec_items, topks, keys=None):
     return res
 
 
+def calculate_metrics_device(ev_keys, lens, rec, topks, n_items):
+    """calculate_metrics (trainer.py:115-144) on the device: `rec` the [users, kmax] int64
+    ranking as the top-k kernel left it, `ev_keys` the sorted (user * n_items + item) keys
+    of the eval lists, `lens` their lengths.  Hits by one searchsorted; hit counts, DCG and
+    ideal DCG for every k from prefix sums along the ranking; the averages over users with a
+    non-empty list in float64.  One small copy to the host at the end (no sync before it)."""
+    n_users, kmax = rec.shape
+    dev = rec.device
+    rk = (torch.arange(n_users, device=dev, dtype=torch.int64)[:, None] * n_items + rec).reshape(-1)
+    if ev_keys.numel():
+        j = torch.searchsorted(ev_keys, rk).clamp_(max=ev_keys.numel() - 1)
+        hit = (ev_keys[j] == rk).view(n_users, kmax).to(torch.float32)
+    else:
+        hit = torch.zeros(n_users, kmax, dtype=torch.float32, device=dev)
+    # the reference's float32 discounts, computed by the same numpy call
+    den = torch.from_numpy(np.log2(np.arange(2, kmax + 2, dtype=np.float32))).to(dev)
+    ks = torch.tensor(list(topks), dtype=torch.int64, device=dev)
+    hit_num = torch.cumsum(hit, 1)[:, ks - 1]                       # [users, n_k]
+    dcg = torch.cumsum(hit / den, 1)[:, ks - 1]
+    lens_f = lens.to(torch.float32)
+    max_hit = torch.minimum(lens.to(torch.int64)[:, None], ks[None, :])
+    ideal = torch.cumsum(1. / den, 0)
+    idcg = ideal[(max_hit - 1).clamp_(min=0)]
+    live = (lens > 0)
+    n_live = live.sum().to(torch.float64)
+    mask = live[:, None].to(torch.float64)
+
+    def avg(x):  # mean over the users with a non-empty eval list
+        return (x.to(torch.float64) * mask).sum(0) / n_live
+    safe_len = torch.where(live, lens_f, torch.ones((), device=dev))[:, None]
+    out = torch.stack([avg(hit_num / ks[None, :].to(torch.float32)), avg(hit_num / safe_len), avg(dcg / idcg)]).cpu().numpy()
+    res = {'Precision': {}, 'Recall': {}, 'NDCG': {}}
+    for c, k in enumerate(topks):
+        res['Precision'][k], res['Recall'][k], res['NDCG'][k] = out[0, c], out[1, c], out[2, c]
+    return res
+
+
 def _csr(lists, n):
     """Per-user lists as (row_ptr, flat items); the iteration runs in C (map / chain)."""
     lists = lists[:n]
@@ -157,6 +194,7 @@ class BasicTrainer:
             if not static:
                 self.__dict__.pop('_excl', None)
                 self.__dict__.pop('_eval_keys', None)
+                self.__dict__.pop('_eval_keys_dev', None)
         self._close_step_graph()  # load() below rebuilds graph structures a captured step points at
         if self.save_path:
             self.model.load(self.save_path)
@@ -229,8 +267,18 @@ class BasicTrainer:
             cache[key] = (eval_data, eval_keys(eval_data, rec_items.shape[0], n_items) + (n_items,))
         return calculate_metrics(eval_data, rec_items, self.topks, keys=cache[key][1])
 
+    def _calculate_metrics_device(self, eval_data, rec):
+        n_items = int(self.dataset.n_items)
+        cache = self.__dict__.setdefault('_eval_keys_dev', {}) if self.static_eval_lists else {}
+        key = (id(eval_data), len(eval_data), rec.shape[0], n_items)
+        if key not in cache:
+            keys, lens = eval_keys(eval_data, rec.shape[0], n_items)
+            cache[key] = (eval_data, torch.from_numpy(keys).to(rec.device), torch.from_numpy(lens).to(rec.device))
+        _, keys, lens = cache[key]
+        return calculate_metrics_device(keys, lens, rec, self.topks, n_items)
+
     @torch.no_grad()
-    def rank(self, val_or_test, banned_items=None):
+    def rank(self, val_or_test, banned_items=None, to_host=True):
         """Top-max(topks) items per user, train items (and val items for
         'test') excluded except for split 'train' (trainer.py:146-170).
         One propagation per eval; per user batch: MFMA score GEMM,
@@ -270,7 +318,8 @@ class BasicTrainer:
                 scores[:, torch.as_tensor(banned_items, device=self.device)] = -np.inf
             _, items = ops.topk(scores, kmax, values=False)
             rec.append(items)  # stays on the device: one copy (and sync) per eval, not per batch
-        return torch.cat(rec).cpu().numpy()
+        rec = torch.cat(rec)
+        return rec.cpu().numpy() if to_host else rec
 
     def eval(self, val_or_test, banned_items=None):
         """trainer.py:146-210; returns the reference's triple (result string,
@@ -283,8 +332,13 @@ class BasicTrainer:
         dropout masks of dropout_rng='cpu' and anything seeded after an eval)."""
         torch.empty((), dtype=torch.int64).random_()
         eval_data = getattr(self.dataset, val_or_test + '_data')
-        rec_items = self.rank(val_or_test, banned_items)
-        metrics = self.calculate_metrics(eval_data, rec_items)
+        if torch.device(self.device).type == 'cuda':
+            # the ranking stays on the device and the metrics are computed there
+            rec_items = self.rank(val_or_test, banned_items, to_host=False)
+            metrics = self._calculate_metrics_device(eval_data, rec_items)
+        else:
+            rec_items = self.rank(val_or_test, banned_items)
+            metrics = self.calculate_metrics(eval_data, rec_items)
         fmt = lambda m: ''.join('{:.3f}, '.format(metrics[m][k] * 100.) for k in self.topks)  # noqa: E731
         results = 'Precision: {:s}Recall: {:s}NDCG: {:s}'.format(fmt('Precision'), fmt('Recall'), fmt('NDCG'))
         return results, metrics, []

@@ -1,70 +1,55 @@
-"""Eval ranking cost breakdown (BasicTrainer.rank, trainer.py:146-182 of the reference):
-score GEMM, train-item mask and top-k per user batch, on ML-1M / Gowalla shaped
-synthetic graphs.  Prints per-stage milliseconds for the whole user set and one JSON line."""
+"""Where one eval (trainer.py:146-210) spends its time at the ML-1M shape: the ranking on the
+GPU (one propagation, score GEMM, mask, top-k, one copy) and the metrics on the host."""
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'inductive-recommendation_amd'))
+sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-SHAPES = {'ml1m': (6040, 3706, 800_000, 64), 'gowalla': (29_858, 40_981, 1_027_370, 128)}
-
-
-def timed(fn, reps=5):
-    fn()
-    torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(reps):
-        fn()
-    b.record()
-    torch.cuda.synchronize()
-    return a.elapsed_time(b) / reps
-
 
 def main():
-    from igr import ops
-    from igr.dataset import synthetic_pairs
+    import ml_like
+    from igr import model as M
+    from igr import trainer as T
+    shape = sys.argv[1] if len(sys.argv) > 1 else 'ml1m_l3'
+    nu, ni, mean_deg, d, L, _ = ml_like.SHAPES[shape]
+    train, val, test = ml_like.make_splits(nu, ni, mean_deg, seed=100)
+
+    class DS:
+        name, n_users, n_items = shape, nu, ni
+        train_data, val_data, test_data = train, val, test
+        train_array = [[u, i] for u in range(nu) for i in train[u]]
+        train_pairs = np.array(train_array, dtype=np.int64)
+
+        def __len__(self):
+            return len(self.train_array)
     dev = torch.device('cuda')
-    out = {}
-    batches = [int(b) for b in (sys.argv[1] if len(sys.argv) > 1 else '512,4096').split(',')]
-    for name, (U, I, E, d) in SHAPES.items():
-        pairs = synthetic_pairs(U, I, E, 0)
-        order = np.lexsort((pairs[:, 1], pairs[:, 0]))
-        p = pairs[order]
-        ptr = torch.from_numpy(np.searchsorted(p[:, 0], np.arange(U + 1)).astype(np.int64)).to(dev)
-        cols = torch.from_numpy(p[:, 1].astype(np.int32)).to(dev)
-        g = torch.Generator(device=dev).manual_seed(0)
-        rep = torch.randn(U + I, d, generator=g, device=dev) * 0.1
-        items = rep[U:]
-        for B in batches:
-            starts = list(range(0, U, B))
-
-            def gemm_all():
-                for s in starts:
-                    ops.gemm(rep[s:min(U, s + B)], items)
-
-            sc = [ops.gemm(rep[s:min(U, s + B)], items) for s in starts]
-
-            def mask_all():
-                for s, x in zip(starts, sc):
-                    ops.mask_scores(x, ptr[s:s + x.shape[0] + 1], cols)
-
-            def topk_all():
-                for x in sc:
-                    ops.topk(x, 100, values=False)
-
-            t_g, t_m, t_k = timed(gemm_all), timed(mask_all), timed(topk_all)
-            flops = 2.0 * U * I * d
-            r = {'gemm_ms': t_g, 'mask_ms': t_m, 'topk_ms': t_k, 'total_ms': t_g + t_m + t_k,
-                 'gemm_tflops': flops / t_g / 1e9, 'topk_GBps': U * I * 4 / t_k / 1e6}
-            out[f'{name}_B{B}'] = r
-            print(name, B, r, file=sys.stderr, flush=True)
-            del sc
-    print(json.dumps(out), flush=True)
+    m = M.IGCN({'name': 'IGCN', 'embedding_size': d, 'n_layers': L, 'device': dev, 'dropout': 0.3, 'feature_ratio': 1.,
+                'dataset': DS()})
+    out = {'shape': shape}
+    for static in (False, True):
+        tr = T.BasicTrainer({'name': 'BasicTrainer', 'dataset': DS(), 'model': m, 'topks': [1, 5, 10, 15, 20],
+                             'device': dev, 'n_epochs': 0, 'test_batch_size': 512, 'static_eval_lists': static})
+        for _ in range(3):
+            tr.eval('test')
+        torch.cuda.synchronize()
+        t = {'rank': 0., 'metrics': 0.}
+        n = 20
+        for _ in range(n):
+            t0 = time.perf_counter()
+            rec = tr.rank('test')
+            t1 = time.perf_counter()
+            tr.calculate_metrics(tr.dataset.test_data, rec)
+            t2 = time.perf_counter()
+            t['rank'] += (t1 - t0) / n
+            t['metrics'] += (t2 - t1) / n
+        out['static_lists' if static else 'lists_read_every_eval'] = {k: round(v * 1e3, 3) for k, v in t.items()}
+    print(json.dumps(out))
 
 
 if __name__ == '__main__':

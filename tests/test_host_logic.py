@@ -19,6 +19,14 @@ def test_vectorised_calculate_metrics_matches_reference_fixture(golden):
     res = T.calculate_metrics(test_data, golden['cm_rec_items'], topks)
     for mk in ['Precision', 'Recall', 'NDCG']:
         np.testing.assert_allclose([res[mk][k] for k in topks], golden['cm_' + mk], rtol=1e-6)
+    # the tensor form eval() uses on the device (here on CPU tensors): prefix sums, float64 averages
+    import torch
+    rec = golden['cm_rec_items']
+    n_items = int(golden['n_items'])
+    keys, lens = T.eval_keys(test_data, rec.shape[0], n_items)
+    res = T.calculate_metrics_device(torch.from_numpy(keys), torch.from_numpy(lens), torch.from_numpy(rec), topks, n_items)
+    for mk in ['Precision', 'Recall', 'NDCG']:
+        np.testing.assert_allclose([res[mk][k] for k in topks], golden['cm_' + mk], rtol=1e-6)
 
 
 def test_bpr_batch_sampler_semantics():

@@ -409,35 +409,73 @@ __global__ __launch_bounds__(NT) void spmm_combine(const int32_t *__restrict__ s
     if (slot == 0) store_row4(epi, split_row[i], sub * 4, red[0][sub]);
 }
 
-// The same for graphs whose split rows have few chunks each (a small graph with a low
-// split threshold: thousands of split rows of 2-3 chunks): a wave per split row, four rows
-// per workgroup, no LDS and no barrier.  The wave's 64 / (D / 4) slots take alternate
-// chunks and are added in a fixed xor tree.
+// The same with a wave per split row, four rows per workgroup, for graphs whose split rows
+// mostly have few chunks (a small graph with a low split threshold: thousands of split
+// rows of 2-3 chunks, for which a workgroup with LDS and barriers per row is the cost).
+// A wave's 64 / (D / 4) slots take alternate chunks and are added in a fixed xor tree.
+// A row of more than kWaveChunks chunks (a hub row; rows come heaviest first, so these
+// fill the first workgroups) is instead added by the whole workgroup as in spmm_combine:
+// the test is uniform over the workgroup.
+constexpr int kWaveChunks = 32;
+
 template <int D>
 __global__ __launch_bounds__(256) void spmm_combine_wave(const int32_t *__restrict__ split_row,
                                                          const int64_t *__restrict__ split_ptr,
                                                          int64_t n_split, const float *__restrict__ ws, Epi epi) {
     constexpr int LPR = D / 4;
-    constexpr int S = 64 / LPR;
-    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= n_split) return;
+    constexpr int S = 64 / LPR;         // slots of a wave
+    constexpr int SB = 4 * S;           // slots of the workgroup
+    __shared__ float4 red[SB][LPR];
+    const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int slot = lane / LPR;
-    const int sub = lane - slot * LPR;
-    const int32_t r = split_row[i];
-    if (epi.row_mask && !bit_set(epi.row_mask, r)) return;  // wave-uniform
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int64_t e = split_ptr[i + 1];
-    for (int64_t c = split_ptr[i] + slot; c < e; c += S)
-        a = f4_add(a, *reinterpret_cast<const float4 *>(ws + c * D + sub * 4));
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {
+        const int64_t i = (int64_t)blockIdx.x * 4 + q;
+        if (i >= n_split) break;  // uniform
+        const int64_t b = split_ptr[i], e = split_ptr[i + 1];
+        const int32_t r = split_row[i];
+        if (epi.row_mask && !bit_set(epi.row_mask, r)) continue;  // uniform
+        if (e - b > kWaveChunks) {
+            // the whole workgroup on this row: 8 independent sums per slot, then a fixed tree
+            const int slot = threadIdx.x / LPR;
+            const int sub = threadIdx.x - slot * LPR;
+            constexpr int V = 8;
+            float4 a[V];
 #pragma unroll
-    for (int m = LPR; m < 64; m <<= 1) {
-        a.x += shfl_xor_f(a.x, m);
-        a.y += shfl_xor_f(a.y, m);
-        a.z += shfl_xor_f(a.z, m);
-        a.w += shfl_xor_f(a.w, m);
+            for (int j = 0; j < V; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            int64_t c = b + slot;
+            for (; c + (V - 1) * SB < e; c += V * SB) {
+#pragma unroll
+                for (int j = 0; j < V; ++j)
+                    a[j] = f4_add(a[j], *reinterpret_cast<const float4 *>(ws + (c + j * SB) * D + sub * 4));
+            }
+            for (; c < e; c += SB) a[0] = f4_add(a[0], *reinterpret_cast<const float4 *>(ws + c * D + sub * 4));
+            __syncthreads();  // red may still be read for the previous heavy row
+            red[slot][sub] = f4_add(f4_add(f4_add(a[0], a[1]), f4_add(a[2], a[3])),
+                                    f4_add(f4_add(a[4], a[5]), f4_add(a[6], a[7])));
+            __syncthreads();
+#pragma unroll
+            for (int w = SB / 2; w >= 1; w >>= 1) {
+                if (slot < w) red[slot][sub] = f4_add(red[slot][sub], red[slot + w][sub]);
+                __syncthreads();
+            }
+            if (slot == 0) store_row4(epi, r, sub * 4, red[0][sub]);
+        } else if (wave == q) {
+            const int slot = lane / LPR;
+            const int sub = lane - slot * LPR;
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int64_t c = b + slot; c < e; c += S)
+                a = f4_add(a, *reinterpret_cast<const float4 *>(ws + c * D + sub * 4));
+#pragma unroll
+            for (int m = LPR; m < 64; m <<= 1) {
+                a.x += shfl_xor_f(a.x, m);
+                a.y += shfl_xor_f(a.y, m);
+                a.z += shfl_xor_f(a.z, m);
+                a.w += shfl_xor_f(a.w, m);
+            }
+            if (slot == 0) store_row4(epi, r, sub * 4, a);
+        }
     }
-    if (slot == 0) store_row4(epi, r, sub * 4, a);
 }
 
 // Any d / alignment: one wave per row, lanes over features.
@@ -486,7 +524,7 @@ static void launch_fast(const igr_csr *g, const float *x, int64_t ldx, const W &
         if (g->n_chunks >= 64 * g->n_split)
             hipLaunchKernelGGL((spmm_combine<D, 1024>), dim3((unsigned)g->n_split), dim3(1024), 0, st, g->split_row,
                                g->split_ptr, g->n_split, ws, epi);
-        else if (g->n_chunks <= 8 * g->n_split)
+        else if (g->n_chunks <= 8 * g->n_split)  // mostly short split rows; hub rows inside take the workgroup
             hipLaunchKernelGGL((spmm_combine_wave<D>), dim3((unsigned)((g->n_split + 3) / 4)), dim3(256), 0, st,
                                g->split_row, g->split_ptr, g->n_split, ws, epi);
         else

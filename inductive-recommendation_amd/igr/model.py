@@ -691,7 +691,9 @@ class IMCGAE(BasicModel):
                 s = s * mask[:, None]
             x = ops.gspmm(self.norm_adj, 'mul', 'sum', x, self.norm_vals)
             with torch.no_grad():
-                s = ops.gspmm(self.norm_adj, 'mul', 'sum', s, self.norm_vals)
+                # one scalar per node, carried 32 wide: the narrowest width of the scheduled SpMM
+                # kernel (the any-width kernel gives a row to one wave, a hub row to one lane)
+                s = ops.gspmm(self.norm_adj, 'mul', 'sum', s.expand(-1, 32).contiguous(), self.norm_vals)[:, :1]
             acc = acc + x / float(i + 2)
             if i % 2 == 0:
                 odd = odd + s / float(i + 2)  # layer i + 1

@@ -93,6 +93,8 @@ def spmm(g: Graph, x, rhs=None, out=None, epi=None):
         if rhs.numel() != g.nnz:
             raise IgrError(f'rhs has {rhs.numel()} values, graph has {g.nnz} edges')
         rhs = rhs.contiguous()
+    if out is None and epi is None and d not in _SCHEDULED_WIDTHS and g.nnz and g.n_rows:
+        return _spmm_other_width(g, x, rhs, d)
     if out is None:
         out = torch.empty(g.n_rows, d, dtype=torch.float32, device=x.device)
     if out.shape[0] < g.n_rows or out.shape[1] != d or out.stride(1) != 1:
@@ -108,6 +110,30 @@ def spmm(g: Graph, x, rhs=None, out=None, epi=None):
     else:
         L.call('igr_spmm_f32', ctypes.byref(g.csr), d, _p(x), ldx, _p(rhs), _p(out), out.stride(0),
                ctypes.byref(epi), None, _stream())
+    return out
+
+
+# Widths the scheduled SpMM kernel is built for.  Any other width goes through it too, in
+# column blocks of these widths with the last one zero-padded: the any-width kernel of the
+# library gives a row to one wave and a feature to one lane, so a hub row at width 1 is one
+# lane's loop (712 us against 20 us on a MovieLens-1M-shaped graph).  Same sums, column by column.
+_SCHEDULED_WIDTHS = (32, 64, 128, 256)
+
+
+def _spmm_other_width(g, x, rhs, d):
+    out = torch.empty(g.n_rows, d, dtype=torch.float32, device=x.device)
+    c = 0
+    while c < d:
+        left = d - c
+        w = 256 if left >= 256 else next(v for v in _SCHEDULED_WIDTHS if v >= left)
+        n = min(w, left)
+        if n == w and c % 4 == 0 and x.stride(0) % 4 == 0 and d % 4 == 0:
+            spmm(g, x[:, c:c + w], rhs, out=out[:, c:c + w])  # a column block in place (16-byte aligned views)
+        else:
+            xp = torch.zeros(x.shape[0], w, dtype=torch.float32, device=x.device)
+            xp[:, :n] = x[:, c:c + n]
+            out[:, c:c + n] = spmm(g, xp, rhs)[:, :n]
+        c += n
     return out
 
 

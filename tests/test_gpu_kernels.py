@@ -56,7 +56,7 @@ def t(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
 
 
-@pytest.mark.parametrize('d', [32, 64, 128, 256, 48, 20])
+@pytest.mark.parametrize('d', [32, 64, 128, 256, 48, 20, 1, 300, 258])
 @pytest.mark.parametrize('skew', [False, True])
 def test_spmm_matches_oracle(d, skew):
     g, v = rand_graph(700, 500, 20000, seed=d, skew=skew, split_threshold=64, chunk_edges=64)
@@ -64,7 +64,11 @@ def test_spmm_matches_oracle(d, skew):
         assert g.n_split > 0 and g.n_chunks > g.n_split  # exercises the chunk tier + combine
     x = np.random.default_rng(9).standard_normal((500, d)).astype(np.float32)
     y = ops.spmm(g, t(x), t(v)).cpu().numpy()
-    close(y, O.spmm64(oracle_csr(g, v), x))
+    ref = O.spmm64(oracle_csr(g, v), x)
+    if d == 1:  # a one-element row has no row scale to bound a cancelling sum against: the tensor's scale
+        assert np.abs(y - ref).max() <= 1e-5 * np.abs(ref).max()
+    else:
+        close(y, ref)
 
 
 def test_spmm_unit_weights_and_empty_rows():

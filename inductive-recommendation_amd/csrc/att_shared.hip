@@ -14,8 +14,10 @@
 //   igr_sddmm_shared_f32        out[eid, h] = < u[r, h, :], v[c, :] >
 //   igr_spmm_shared_heads_f32   y[r, h, :]  = sum_{e in row r} rhs[eid, h] * x[c, :]
 //                               (its gradient with respect to u)
-// Both: one wave per destination row, d / 4 lanes per source row (one 16-byte load
-// per lane), 64 / (d / 4) edges side by side, several edges per lane group in flight.
+// Both: a wave per destination row - or, following the graph's row schedule, per chunk of
+// a split row and per unsplit row, heaviest first (a hub row is otherwise one wave's
+// loop) - d / 4 lanes per source row (one 16-byte load per lane), 64 / (d / 4) edges side
+// by side, several edges per lane group in flight.
 #include "common.h"
 
 namespace igr {

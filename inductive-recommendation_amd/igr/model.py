@@ -131,6 +131,17 @@ class BasicModel(nn.Module):
     def predict(self, users):
         raise NotImplementedError
 
+    def _join_batch_stream(self, *tensors):
+        """A caller that drew the batch on another stream (trainer.StepGraph: the sampling then
+        runs beside the propagation, which does not read it) leaves that stream in
+        `_batch_stream`; the current stream waits for it here, just before the batch's first use."""
+        bs = self.__dict__.pop('_batch_stream', None)
+        if bs is not None:
+            cur = torch.cuda.current_stream()
+            cur.wait_stream(bs)
+            for t in tensors:
+                t.record_stream(cur)
+
     def save(self, path):
         torch.save(self.state_dict(), path)
 
@@ -183,12 +194,14 @@ class LightGCN(BasicModel):
         (a trainer whose l2_reg is 0: the term and its gradient are exact zeros) skips
         the l2 pass and returns None for it."""
         if batch_rep_pays(self, users.numel()):
+            self._join_batch_stream(users, pos_items, neg_items)
             rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
             rep_b = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
                                        adj_vals=self.norm_vals)
             bpr, _ = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0, distinct=True)
         else:
             rep = self.get_rep()
+            self._join_batch_stream(users, pos_items, neg_items)
             bpr, _ = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
         if not need_l2:
             return bpr, None
@@ -456,12 +469,15 @@ class IGCN(BasicModel):
         (l2_reg = 0, as in the reference's IGCN configs: the term and its gradient are
         exact zeros) returns None for l2 and skips AttIGCN's projection norms."""
         if self._rows_path(users.numel()):
+            self._join_batch_stream(users, pos_items, neg_items)
             rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
             rep_b = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
                                        feat=self.feat_mat, fvals=self.inductive_values(), adj_vals=self.norm_vals)
             bpr, l2 = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0, distinct=True)
         else:
-            bpr, l2 = ops.bpr_loss(self.get_rep(), users, pos_items, neg_items, 0, self.n_users)
+            rep = self.get_rep()
+            self._join_batch_stream(users, pos_items, neg_items)
+            bpr, l2 = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
         if not need_l2:
             return bpr, None
         extra = self._l2_extra()
@@ -480,6 +496,9 @@ class IGCN(BasicModel):
             # bookkeeping, its backward) runs on a second stream beside the propagation
             cur = torch.cuda.current_stream()
             side.wait_stream(cur)
+            drawn_on = getattr(self, '_batch_stream', None)  # the batches' stream, if not this one's
+            if drawn_on is not None and drawn_on is not side:
+                side.wait_stream(drawn_on)
             with torch.cuda.stream(side):
                 for t in (a_users, a_pos, a_neg):
                     t.record_stream(side)
@@ -488,6 +507,7 @@ class IGCN(BasicModel):
             cur.wait_stream(side)
             aux.record_stream(cur)
             return bpr, l2, aux
+        self._join_batch_stream(users, pos_items, neg_items, a_users, a_pos, a_neg)
         rows, (iu, ip, ineg) = ops.batch_rows(users, pos_items, neg_items, self.n_users)
         rep_b, aux = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
                                         feat=self.feat_mat, fvals=self.inductive_values(), adj_vals=self.norm_vals,

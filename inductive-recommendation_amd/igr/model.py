@@ -477,7 +477,12 @@ class IGCN(BasicModel):
         else:
             rep = self.get_rep()
             self._join_batch_stream(users, pos_items, neg_items)
-            bpr, l2 = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
+            keys = self.__dict__.pop('_bpr_keys', None)  # sorted on the aux stream (bpr_aux_loss)
+            if keys is not None:
+                cur = torch.cuda.current_stream()
+                cur.wait_stream(self._aux_side)
+                keys.record_stream(cur)
+            bpr, l2 = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users, keys=keys)
         if not need_l2:
             return bpr, None
         extra = self._l2_extra()
@@ -502,6 +507,12 @@ class IGCN(BasicModel):
             with torch.cuda.stream(side):
                 for t in (a_users, a_pos, a_neg):
                     t.record_stream(side)
+                if self.training and torch.is_grad_enabled():
+                    # the sort the main term's backward walks depends on the batch alone: done here,
+                    # beside the propagation, instead of between the loss and its gradient
+                    for t in (users, pos_items, neg_items):
+                        t.record_stream(side)
+                    self._bpr_keys = ops.rowsort(users, 0, pos_items, self.n_users, neg_items, self.n_users)
                 aux = self.aux_loss(a_users, a_pos, a_neg)
             bpr, l2 = self.bpr_loss(users, pos_items, neg_items, need_l2)
             cur.wait_stream(side)

@@ -1003,7 +1003,7 @@ class BPRLoss(torch.autograd.Function):
     rows gathered from one table t (model.py:4046-4052, trainer.py:536-548)."""
 
     @staticmethod
-    def forward(ctx, t, w, users, pos, neg, off_u, off_i, distinct):
+    def forward(ctx, t, w, users, pos, neg, off_u, off_i, distinct, keys=None):
         _dev(t, users, pos, neg, w)
         t = t.contiguous()
         B = users.numel()
@@ -1014,6 +1014,7 @@ class BPRLoss(torch.autograd.Function):
         ctx.save_for_backward(t, w, users, pos, neg)
         ctx.off = (int(off_u), int(off_i))
         ctx.distinct = bool(distinct)
+        ctx.keys = keys
         m = means(loss, l2)  # both means in one launch, fixed summation order
         return m[0], m[1]
 
@@ -1028,10 +1029,10 @@ class BPRLoss(torch.autograd.Function):
         dw = torch.zeros_like(w) if (w is not None and ctx.needs_input_grad[1]) else None
         keys = None
         if grad is not None and not ctx.distinct:
-            keys = rowsort(users, ctx.off[0], pos, ctx.off[1], neg, ctx.off[1])
+            keys = ctx.keys if ctx.keys is not None else rowsort(users, ctx.off[0], pos, ctx.off[1], neg, ctx.off[1])
         _bpr_call(B, t.shape[1], users, pos, neg, ctx.off[0], ctx.off[1], t, w, None, None,
                   0.0 if gl is None else 1.0 / B, 0.0 if g2 is None else 1.0 / B, gl, g2, grad, t.stride(0), dw, keys)
-        return grad, dw, None, None, None, None, None, None
+        return grad, dw, None, None, None, None, None, None, None
 
 
 def means(a, b=None):
@@ -1055,12 +1056,14 @@ def loss_combine(bpr, l2=None, aux=None, c_l2=0.0, c_aux=0.0, loss_sum=None, wei
     return out
 
 
-def bpr_loss(t, users, pos, neg, off_u, off_i, w=None, distinct=False):
+def bpr_loss(t, users, pos, neg, off_u, off_i, w=None, distinct=False, keys=None):
     """Returns (mean softplus BPR loss, mean squared-norm term).  distinct: the
     caller guarantees that the 3B table rows read are all different (a table of
-    gathered batch rows read at batch_positions), so the gradient needs no sort."""
+    gathered batch rows read at batch_positions), so the gradient needs no sort.
+    keys: rowsort(users, off_u, pos, off_i, neg, off_i) when the caller already has it
+    (the backward then skips its sort)."""
     return BPRLoss.apply(t, w, users.to(torch.int64).contiguous(), pos.to(torch.int64).contiguous(),
-                         neg.to(torch.int64).contiguous(), off_u, off_i, distinct)
+                         neg.to(torch.int64).contiguous(), off_u, off_i, distinct, keys)
 
 
 # ------------------------------------------------------------------ DGL-compatible API

@@ -1150,3 +1150,59 @@ def test_attention_kernels_split_rows_against_whole_rows(dedup):
         L.call('igr_att_softmax_bwd_f32', ctypes.byref(cut.csr), h, P(a), P(kp), float(sd), P(rmax), P(rsum), P(dw), P(da), st)
         gr = da.cpu().numpy().astype(np.float64)
         assert np.all(np.abs(gr - g0) <= 1e-4 * np.abs(g0) + 1e-5 * np.abs(g0).max())
+
+
+@pytest.mark.parametrize('seed', range(16))
+def test_random_shapes_and_schedules_match_oracle(seed):
+    """Shapes, degree distributions, duplicate edges, widths and row schedules drawn at random
+    (the automatic schedule included): SpMM both ways, the shared-head SDDMM and the edge
+    softmax against the oracle on the same inputs."""
+    rng = np.random.default_rng(1000 + seed)
+    n_rows, n_cols = int(rng.integers(1, 4000)), int(rng.integers(1, 4000))
+    nnz = int(rng.integers(0, 150000))
+    skew, dedup = bool(rng.integers(2)), bool(rng.integers(2))
+    plan = {} if rng.integers(3) == 0 else dict(split_threshold=int(rng.choice([16, 48, 64, 256, 512, 1 << 30])),
+                                                chunk_edges=int(rng.choice([64, 128, 192, 512, 4096])))
+    d = int(rng.choice([32, 64, 128, 256, int(rng.integers(1, 300))]))
+    print(f'seed {seed}: {n_rows} x {n_cols}, nnz {nnz}, skew {skew}, dedup {dedup}, plan {plan}, d {d}', flush=True)
+    g, v = rand_graph(n_rows, n_cols, nnz, seed=seed, skew=skew, dedup=dedup, **plan)
+    A = oracle_csr(g, v)
+    x = rng.standard_normal((n_cols, d)).astype(np.float32)
+    y = ops.spmm(g, t(x), t(v)).cpu().numpy()
+    ref = O.spmm64(A, x)
+    bound = 1e-5 * np.abs(ref) + 2e-6 * max(np.abs(ref).max(initial=0.), 1e-30)  # tensor scale: d may be 1
+    assert np.all(np.abs(y - ref) <= bound)
+    # the transposed product, as the backward takes it: the reverse graph reads values by edge id
+    r = g.reverse()
+    gy = rng.standard_normal((n_rows, d)).astype(np.float32)
+    gx = ops.spmm(r, t(gy), t(v)).cpu().numpy()
+    hr = r.host()
+    At = O.CSR(n_cols, n_rows, hr['row_ptr'], hr['col_idx'].astype(np.int64), v[hr['edge_id']])
+    ref = O.spmm64(At, gy)
+    bound = 1e-5 * np.abs(ref) + 2e-6 * max(np.abs(ref).max(initial=0.), 1e-30)
+    assert np.all(np.abs(gx - ref) <= bound)
+    if g.nnz == 0:
+        return
+    # attention edge kernels (widths the shared-head kernels are built for)
+    h, da = (4, 64) if seed % 2 else (1, 32)
+    q = rng.standard_normal((n_rows, h * da)).astype(np.float32)
+    k = rng.standard_normal((n_cols, da)).astype(np.float32)
+    s = ops.sddmm_shared(g, t(q), t(k), h).cpu().numpy().reshape(g.nnz, h)
+    rows = A.rows()
+    qq = q.reshape(n_rows, h, da)[rows].astype(np.float64)
+    kk = k[A.col].astype(np.float64)[:, None, :]
+    s64, mag = (qq * kk).sum(-1), np.abs(qq * kk).sum(-1)
+    eid = g.host()['edge_id']
+    s_csr = s if eid is None else s[eid]  # per-edge outputs are in edge-id order
+    assert np.all(np.abs(s_csr - s64) <= da * 2.0 ** -23 * mag + 1e-30)
+    alpha = (rng.standard_normal((g.nnz, h)) * 30).astype(np.float32)
+    w = ops.att_softmax(g, t(alpha), ops.sqrt_scale(da))[0].cpu().numpy()
+    a_csr = alpha if eid is None else alpha[eid]
+    w_ref = O.att_softmax(A, a_csr, da)
+    close(w if eid is None else w[eid], w_ref, rtol=2e-5)
+    rhs = rng.standard_normal((g.nnz, h)).astype(np.float32)
+    yh = ops.spmm_shared_heads(g, t(k), t(rhs), h).cpu().numpy()
+    r_csr = rhs if eid is None else rhs[eid]
+    for j in range(h):
+        ref = O.spmm64(O.CSR(n_rows, n_cols, A.row_ptr, A.col, np.ascontiguousarray(r_csr[:, j])), k)
+        close(yh[:, j * da:(j + 1) * da], ref, atol_row=2e-6)

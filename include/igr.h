@@ -423,7 +423,7 @@ int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int64_t lda, i
  * streamed over the m node rows with the dW block held in MFMA accumulators; partial
  * blocks of row ranges go to `workspace` (igr_linear_wgrad_workspace_size bytes, 16-byte
  * aligned) and are added in range order (the same bits on every run).  db nullable.
- * Supported: k_in in {32, 64}, n_out in {64, 128} or a multiple of 256, dy / x 16-byte
+ * Supported: k_in in {32, 64, 128}, n_out in {64, 128} or a multiple of 256, dy / x 16-byte
  * aligned with leading dimensions a multiple of 4; other shapes: igr_gemm_f32 (trans_a). */
 int64_t igr_linear_wgrad_workspace_size(int64_t m, int32_t n_out, int32_t k_in);
 int igr_linear_wgrad_f32(int64_t m, int32_t n_out, int32_t k_in, const float *dy, int64_t ld_dy, const float *x,

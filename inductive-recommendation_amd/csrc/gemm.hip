@@ -471,12 +471,13 @@ extern "C" int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int
 #define IGR_GEMM128 1
 #endif
         // the register-resident-weight kernel: short K, N in whole 64-column groups
-        const bool rows_ok = !trans_a && S == 1 && (k == 32 || k == 64) && n % 64 == 0 && m >= 1024 &&
+        const bool rows_ok = !trans_a && S == 1 && (k == 32 || k == 64 || k == 128) && n % 64 == 0 && m >= 1024 &&
                              lda % 4 == 0 && ldc % 4 == 0 && aligned16(a) && aligned16(c) && n / 64 <= 65535;
         if (rows_ok) {
             const int64_t tiles = (m + 63) / 64;
             // wider column groups per workgroup once there are enough row tiles to fill the chip
-            const int nb = (n % 256 == 0 && tiles >= 512) ? 4 : ((n % 128 == 0 && tiles * 2 >= 512) ? 2 : 1);
+            int nb = (n % 256 == 0 && tiles >= 512) ? 4 : ((n % 128 == 0 && tiles * 2 >= 512) ? 2 : 1);
+            if (k == 128 && nb > 2) nb = 2;  // twice the weight registers per column group
             static int cus = 0;
             if (cus <= 0) {
                 int dev = 0;
@@ -496,7 +497,9 @@ extern "C" int igr_gemm_f32(int64_t m, int64_t n, int64_t k, const float *a, int
             hipLaunchKernelGGL((gemm_rows_persistent<KS_, NB_, false>), gp, dim3(256), 0, st, m, a, lda, b, ldb,  \
                                bias, c, ldc);                                                                     \
     } while (0)
-            if (k == 64) {
+            if (k == 128) {
+                if (nb == 2) IGR_GEMMP(32, 2); else IGR_GEMMP(32, 1);
+            } else if (k == 64) {
                 if (nb == 4) IGR_GEMMP(16, 4); else if (nb == 2) IGR_GEMMP(16, 2); else IGR_GEMMP(16, 1);
             } else {
                 if (nb == 4) IGR_GEMMP(8, 4); else if (nb == 2) IGR_GEMMP(8, 2); else IGR_GEMMP(8, 1);

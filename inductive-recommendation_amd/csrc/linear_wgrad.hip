@@ -2,7 +2,7 @@
 //
 //   dW[n, c] = sum_m dy[m, n] * x[m, c],   db[n] = sum_m dy[m, n]
 //
-// for y = x W^T + b with M = node count rows, k_in in {32, 64} input columns and
+// for y = x W^T + b with M = node count rows, k_in in {32, 64, 128} input columns and
 // n_out a multiple of 64 (NGCF's Linear(d, d), model.py:4039, and AttIGCN's
 // Linear(d, 4d), model.py:4259, 4264 - the backward of loss.backward(), trainer.py:553).
 // As a GEMM this is a few output tiles with K = node count; here it is a stream:
@@ -46,7 +46,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 #endif
 constexpr int WG_PF = IGR_WGRAD_PF;  // k steps (of 4 data rows) whose loads are issued before their MFMAs
 
-// NT = k_in / 16 column tiles (4: float4 of x per lane, 2: float2)
+// NT = k_in / 16 column tiles (8: two float4 of x per lane, 4: float4, 2: float2)
 template <int NT>
 __global__ __launch_bounds__(256, IGR_WGRAD_OCC) void linear_wgrad_kernel(int64_t M, int n_out, int nb_in_wg,
                                                            const float *__restrict__ dy, int64_t ld_dy,
@@ -87,7 +87,15 @@ __global__ __launch_bounds__(256, IGR_WGRAD_OCC) void linear_wgrad_kernel(int64_
             const int64_t m = gb + 4 * s + kk;
             const int64_t mc = (!CLAMP || m < M) ? m : M - 1;
             a[s] = *reinterpret_cast<const f32x4 *>(dyp + mc * ld_dy);
-            if (NT == 4) {
+            if (NT == 8) {
+                const f32x4 v0 = *reinterpret_cast<const f32x4 *>(xp + mc * ld_x);
+                const f32x4 v1 = *reinterpret_cast<const f32x4 *>(xp + mc * ld_x + 4);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    b[s][u] = v0[u];
+                    b[s][4 + u] = v1[u];
+                }
+            } else if (NT == 4) {
                 const f32x4 v = *reinterpret_cast<const f32x4 *>(xp + mc * ld_x);
 #pragma unroll
                 for (int u = 0; u < NT; ++u) b[s][u] = v[u];
@@ -155,7 +163,11 @@ __global__ __launch_bounds__(256, IGR_WGRAD_OCC) void linear_wgrad_kernel(int64_
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             float *o = pw + (int64_t)(4 * (4 * kk + r) + t) * KIN + NT * i16;
-            if (NT == 4)
+            if (NT == 8) {
+                *reinterpret_cast<f32x4 *>(o) = f32x4{acc[t][0][r], acc[t][1][r], acc[t][2][r], acc[t][3][r]};
+                *reinterpret_cast<f32x4 *>(o + 4) =
+                    f32x4{acc[t][NT - 4][r], acc[t][NT - 3][r], acc[t][NT - 2][r], acc[t][NT - 1][r]};
+            } else if (NT == 4)
                 *reinterpret_cast<f32x4 *>(o) = f32x4{acc[t][0][r], acc[t][1][r], acc[t][2][r], acc[t][3][r]};
             else
                 *reinterpret_cast<f32x2 *>(o) = f32x2{acc[t][0][r], acc[t][NT - 1][r]};
@@ -214,7 +226,7 @@ static int64_t wgrad_ranges(int64_t m, int32_t n_out) {
 
 static bool wgrad_shape_ok(int64_t m, int32_t n_out, int32_t k_in) {
     const int nb = n_out / 64;
-    return m > 0 && n_out > 0 && n_out % 64 == 0 && (k_in == 32 || k_in == 64) &&
+    return m > 0 && n_out > 0 && n_out % 64 == 0 && (k_in == 32 || k_in == 64 || k_in == 128) &&
            (nb == 1 || nb == 2 || nb % 4 == 0);
 }
 
@@ -233,7 +245,7 @@ extern "C" int igr_linear_wgrad_f32(int64_t m, int32_t n_out, int32_t k_in, cons
     return guarded("igr_linear_wgrad_f32", [&]() -> int {
         const char *fn = "igr_linear_wgrad_f32";
         if (!wgrad_shape_ok(m, n_out, k_in))
-            return arg_error(fn, "supported: k_in in {32, 64}, n_out in {64, 128} or a multiple of 256, m > 0");
+            return arg_error(fn, "supported: k_in in {32, 64, 128}, n_out in {64, 128} or a multiple of 256, m > 0");
         if (!dy || !x || !dw) return arg_error(fn, "NULL pointer");
         if (ld_dy < n_out || ld_x < k_in || ld_dw < k_in) return arg_error(fn, "leading dimension too small");
         if (ld_dy % 4 || ld_x % 4 || !aligned16(dy) || !aligned16(x))
@@ -249,7 +261,10 @@ extern "C" int igr_linear_wgrad_f32(int64_t m, int32_t n_out, int32_t k_in, cons
         float *part = static_cast<float *>(workspace);
         float *part_b = db ? part + ranges * (int64_t)n_out * k_in : nullptr;
         const dim3 grid((unsigned)((ranges + ranges_in_wg - 1) / ranges_in_wg), (unsigned)(nb / nb_in_wg));
-        if (k_in == 64)
+        if (k_in == 128)
+            hipLaunchKernelGGL((linear_wgrad_kernel<8>), grid, dim3(256), 0, st, m, (int)n_out, nb_in_wg, dy, ld_dy, x,
+                               ld_x, ranges, part, part_b);
+        else if (k_in == 64)
             hipLaunchKernelGGL((linear_wgrad_kernel<4>), grid, dim3(256), 0, st, m, (int)n_out, nb_in_wg, dy, ld_dy, x,
                                ld_x, ranges, part, part_b);
         else

@@ -906,7 +906,9 @@ def test_gemm_128_tiles_every_transposition(m, n, k):
 
 @pytest.mark.parametrize('m,n,k,tb', [(4133, 256, 64, False), (1024, 64, 64, True), (33001, 256, 64, False),
                                       (40000, 128, 32, False), (70000, 512, 64, True), (20011, 64, 32, False),
-                                      (17000, 128, 64, False), (1100002, 256, 64, False)])
+                                      (17000, 128, 64, False), (1100002, 256, 64, False),
+                                      (70839, 512, 128, False), (5003, 128, 128, True), (1500, 64, 128, False),
+                                      (40001, 256, 128, True)])
 def test_gemm_register_resident_weight_kernel(m, n, k, tb):
     """The persistent projection kernel (weight slice in registers, transposed MFMA,
     direct 16-byte C stores): short K, N in 64-column groups, M tails, every
@@ -989,7 +991,8 @@ def test_loss_combine_is_the_reference_expression_bitwise():
 
 
 @pytest.mark.parametrize('m,n_out,k_in', [(9748, 256, 64), (1000, 64, 64), (33001, 128, 32), (70, 64, 32), (31, 64, 64),
-                                          (4133, 512, 64), (20011, 64, 32), (1100002, 256, 64)])
+                                          (4133, 512, 64), (20011, 64, 32), (1100002, 256, 64),
+                                          (70839, 512, 128), (5003, 128, 128), (50, 64, 128)])
 def test_linear_wgrad_streamed(m, n_out, k_in):
     """dW = dy^T x and db = column sums of dy in one streamed pass (operands straight from
     global memory into the MFMAs, partial blocks of row ranges added in order): against

@@ -514,7 +514,10 @@ class IGCN(BasicModel):
                         t.record_stream(side)
                     self._bpr_keys = ops.rowsort(users, 0, pos_items, self.n_users, neg_items, self.n_users)
                 aux = self.aux_loss(a_users, a_pos, a_neg)
-            bpr, l2 = self.bpr_loss(users, pos_items, neg_items, need_l2)
+            try:
+                bpr, l2 = self.bpr_loss(users, pos_items, neg_items, need_l2)
+            finally:
+                self.__dict__.pop('_bpr_keys', None)  # never left for a later, different batch
             cur.wait_stream(side)
             aux.record_stream(cur)
             return bpr, l2, aux

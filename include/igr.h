@@ -488,6 +488,23 @@ int igr_adam_multi_f32(int32_t n_slots, const igr_adam_slot *slots, double lr, d
  * captured training step advances at its end). */
 int igr_counter_add(int64_t *counter, int64_t value, void *stream);
 
+/* NGCF layer tail (reference model.py:4040-4042, after the two Linear layers):
+ *   r   = dropout(leaky_relu(a + b, slope))     keep: 0/1 per element ([n, d], NULL = no
+ *                                               dropout), kept elements times keep_scale
+ *   nrm = r / max(|r|_2, 1e-12) per row         (F.normalize, written with leading dim ldn,
+ *                                               e.g. into a column block of the concatenation)
+ * row_norm[n] receives the clamped row norms for the backward.  a, b: [n, d] with leading
+ * dimensions lda, ldb; r: [n, d] contiguous; 0 < d <= 256. */
+int igr_layer_tail_f32(int64_t n, int32_t d, const float *a, int64_t lda, const float *b, int64_t ldb,
+                       const float *keep, float keep_scale, float slope, float *r, float *nrm, int64_t ldn,
+                       float *row_norm, void *stream);
+/* Its gradient (loss.backward(), reference trainer.py:426): dz = d loss / d (a + b) from
+ * gn = d loss / d nrm and gr = d loss / d r (either may be NULL), with r and row_norm of the
+ * forward.  dz: [n, d] contiguous; it is the gradient of both a and b. */
+int igr_layer_tail_bwd_f32(int64_t n, int32_t d, const float *gn, int64_t ldgn, const float *gr, int64_t ldgr,
+                           const float *r, const float *row_norm, const float *keep, float keep_scale,
+                           float slope, float *dz, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -318,3 +318,145 @@ extern "C" int igr_counter_add(int64_t *counter, int64_t value, void *stream) {
         return launch_status("igr_counter_add");
     });
 }
+
+// ---- NGCF layer tail (model.py:4040-4042): r = dropout(leaky_relu(a + b)), nrm = r / max(|r|_2, eps)
+// One wave per node row, lane l holds columns l, l + 64, ... (V of them): one coalesced read of
+// a and b, one write of r and nrm; the row norm is a wave reduction.  keep (0/1 per element,
+// NULL in eval mode) times keep_scale = 1 / (1 - p) is the dropout mask.
+namespace igr {
+
+constexpr float kNormEps = 1e-12f;  // F.normalize's eps
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_f(v, m);
+    return v;
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void layer_tail_kernel(int64_t n, int d, const float *__restrict__ a, int64_t lda,
+                                                         const float *__restrict__ b, int64_t ldb,
+                                                         const float *__restrict__ keep, float keep_scale, float slope,
+                                                         float *__restrict__ r, float *__restrict__ nrm, int64_t ldn,
+                                                         float *__restrict__ row_norm) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;  // whole waves leave; no barrier below
+    float y[V];
+    float ss = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int c = lane + 64 * v;
+        y[v] = 0.f;
+        if (c < d) {
+            const float z = a[row * lda + c] + b[row * ldb + c];
+            float t = z > 0.f ? z : z * slope;
+            if (keep) t = t * keep[row * d + c] * keep_scale;
+            y[v] = t;
+            ss += t * t;
+        }
+    }
+    const float nr = fmaxf(sqrtf(wave_sum(ss)), kNormEps);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int c = lane + 64 * v;
+        if (c < d) {
+            r[row * d + c] = y[v];
+            nrm[row * ldn + c] = y[v] / nr;
+        }
+    }
+    if (lane == 0) row_norm[row] = nr;
+}
+
+// gradient of the tail: gn = d loss / d nrm, gr = d loss / d r (either may be NULL), both added;
+// dz = d loss / d (a + b).  The normalisation's clamp passes no gradient through the norm.
+template <int V>
+__global__ __launch_bounds__(256) void layer_tail_bwd_kernel(int64_t n, int d, const float *__restrict__ gn, int64_t ldgn,
+                                                             const float *__restrict__ gr, int64_t ldgr,
+                                                             const float *__restrict__ r,
+                                                             const float *__restrict__ row_norm,
+                                                             const float *__restrict__ keep, float keep_scale,
+                                                             float slope, float *__restrict__ dz) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const float nr = row_norm[row];
+    float rv[V], g[V];
+    float dot = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int c = lane + 64 * v;
+        rv[v] = g[v] = 0.f;
+        if (c < d) {
+            rv[v] = r[row * d + c];
+            if (gn) {
+                g[v] = gn[row * ldgn + c];
+                dot += g[v] * rv[v];
+            }
+        }
+    }
+    // nrm = r / nr: d/dr = (gn - nrm <gn, nrm>) / nr above the clamp, gn / nr on it
+    const float proj = nr > kNormEps ? wave_sum(dot) / (nr * nr) : 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int c = lane + 64 * v;
+        if (c < d) {
+            float t = gn ? (g[v] - rv[v] * proj) / nr : 0.f;
+            if (gr) t += gr[row * ldgr + c];
+            if (keep) t = t * keep[row * d + c] * keep_scale;
+            dz[row * d + c] = rv[v] > 0.f ? t : t * slope;
+        }
+    }
+}
+
+}  // namespace igr
+
+static bool tail_args_ok(const char *fn, int64_t n, int32_t d) {
+    if (n < 0 || d <= 0 || d > 256) {
+        arg_error(fn, "need n >= 0 and 0 < d <= 256");
+        return false;
+    }
+    return true;
+}
+
+extern "C" int igr_layer_tail_f32(int64_t n, int32_t d, const float *a, int64_t lda, const float *b, int64_t ldb,
+                                  const float *keep, float keep_scale, float slope, float *r, float *nrm, int64_t ldn,
+                                  float *row_norm, void *stream) {
+    return guarded("igr_layer_tail_f32", [&]() -> int {
+        const char *fn = "igr_layer_tail_f32";
+        if (!tail_args_ok(fn, n, d)) return IGR_ERR_ARG;
+        if (n == 0) return IGR_OK;
+        if (!a || !b || !r || !nrm || !row_norm) return arg_error(fn, "NULL pointer");
+        if (lda < d || ldb < d || ldn < d) return arg_error(fn, "leading dimension too small");
+        if ((n + 3) / 4 > 2147483647) return arg_error(fn, "too many rows");
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        const dim3 grid((unsigned)((n + 3) / 4));
+#define IGR_TAIL(V_)                                                                                             \
+    hipLaunchKernelGGL((layer_tail_kernel<V_>), grid, dim3(256), 0, st, n, (int)d, a, lda, b, ldb, keep, keep_scale, \
+                       slope, r, nrm, ldn, row_norm)
+        if (d <= 64) IGR_TAIL(1); else if (d <= 128) IGR_TAIL(2); else IGR_TAIL(4);
+#undef IGR_TAIL
+        return launch_status(fn);
+    });
+}
+
+extern "C" int igr_layer_tail_bwd_f32(int64_t n, int32_t d, const float *gn, int64_t ldgn, const float *gr, int64_t ldgr,
+                                      const float *r, const float *row_norm, const float *keep, float keep_scale,
+                                      float slope, float *dz, void *stream) {
+    return guarded("igr_layer_tail_bwd_f32", [&]() -> int {
+        const char *fn = "igr_layer_tail_bwd_f32";
+        if (!tail_args_ok(fn, n, d)) return IGR_ERR_ARG;
+        if (n == 0) return IGR_OK;
+        if (!r || !row_norm || !dz) return arg_error(fn, "NULL pointer");
+        if ((gn && ldgn < d) || (gr && ldgr < d)) return arg_error(fn, "leading dimension too small");
+        if ((n + 3) / 4 > 2147483647) return arg_error(fn, "too many rows");
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        const dim3 grid((unsigned)((n + 3) / 4));
+#define IGR_TAILB(V_)                                                                                              \
+    hipLaunchKernelGGL((layer_tail_bwd_kernel<V_>), grid, dim3(256), 0, st, n, (int)d, gn, ldgn, gr, ldgr, r, row_norm, \
+                       keep, keep_scale, slope, dz)
+        if (d <= 64) IGR_TAILB(1); else if (d <= 128) IGR_TAILB(2); else IGR_TAILB(4);
+#undef IGR_TAILB
+        return launch_status(fn);
+    });
+}

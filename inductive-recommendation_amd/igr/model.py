@@ -262,9 +262,13 @@ class NGCF(BasicModel):
             m1 = representations * m0
             m0 = ops.linear(m0, self.gc_layers[layer_idx])
             m1 = ops.linear(m1, self.bi_layers[layer_idx])
-            representations = F.leaky_relu(m0 + m1, negative_slope=0.2)
-            representations = F.dropout(representations, p=self.dropout, training=self.training)
-            all_layer_rep.append(F.normalize(representations, p=2, dim=1))
+            if m0.shape[1] <= ops.LAYER_TAIL_MAX_WIDTH:  # activation, dropout and row norm in one kernel
+                representations, normed = ops.layer_tail(m0, m1, self.dropout, self.training, slope=0.2)
+            else:
+                representations = F.leaky_relu(m0 + m1, negative_slope=0.2)
+                representations = F.dropout(representations, p=self.dropout, training=self.training)
+                normed = F.normalize(representations, p=2, dim=1)
+            all_layer_rep.append(normed)
         return torch.cat(all_layer_rep, dim=1)
 
     def bpr_forward(self, users, pos_items, neg_items):
@@ -274,6 +278,14 @@ class NGCF(BasicModel):
         pos_r, neg_r = ops.gather(rep, pos_items, self.n_users), ops.gather(rep, neg_items, self.n_users)
         l2_norm_sq = (users_r ** 2).sum(1) + (pos_r ** 2).sum(1) + (neg_r ** 2).sum(1)
         return users_r, pos_r, neg_r, l2_norm_sq
+
+    def bpr_loss(self, users, pos_items, neg_items, need_l2=True):
+        """Fused BPRTrainer step terms (trainer.py:410-421 over model.py:4046-4052): (bpr loss,
+        mean l2 of the gathered rep rows) from one pass over the batch's rep rows."""
+        rep = self.get_rep()
+        self._join_batch_stream(users, pos_items, neg_items)
+        bpr, l2 = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
+        return bpr, (l2 if need_l2 else None)
 
     def predict(self, users, rep=None):
         return LightGCN.predict(self, users, rep)
@@ -744,6 +756,9 @@ class IMCGAE(BasicModel):
 
     def bpr_forward(self, users, pos_items, neg_items):
         return NGCF.bpr_forward(self, users, pos_items, neg_items)
+
+    def bpr_loss(self, users, pos_items, neg_items, need_l2=True):
+        return NGCF.bpr_loss(self, users, pos_items, neg_items, need_l2)
 
     def predict(self, users, rep=None):
         return LightGCN.predict(self, users, rep)

@@ -708,6 +708,60 @@ def gather(src, idx, offset=0):
     return GatherRows.apply(src, idx, int(offset))
 
 
+LAYER_TAIL_MAX_WIDTH = 256
+
+
+class LayerTail(torch.autograd.Function):
+    """NGCF's layer tail after the two Linear layers (model.py:4040-4042) in one kernel each way:
+    r = dropout(leaky_relu(a + b)), nrm = F.normalize(r, p=2, dim=1); returns (r, nrm)."""
+
+    @staticmethod
+    def forward(ctx, a, b, keep, keep_scale, slope):
+        _dev(a, b, keep)
+        a, lda = _rows(a)
+        b, ldb = _rows(b)
+        n, d = a.shape
+        if b.shape != a.shape or (keep is not None and keep.shape != a.shape):
+            raise IgrError(f'layer_tail: a {tuple(a.shape)}, b {tuple(b.shape)}')
+        keep = None if keep is None else _f32(keep).contiguous()
+        r = torch.empty(n, d, dtype=torch.float32, device=a.device)
+        nrm = torch.empty_like(r)
+        row_norm = torch.empty(n, dtype=torch.float32, device=a.device)
+        L.call('igr_layer_tail_f32', n, d, _p(a), lda, _p(b), ldb, _p(keep), float(keep_scale), float(slope), _p(r),
+               _p(nrm), d, _p(row_norm), _stream())
+        ctx.save_for_backward(r, row_norm, keep)
+        ctx.consts = (float(keep_scale), float(slope))
+        ctx.set_materialize_grads(False)
+        return r, nrm
+
+    @staticmethod
+    def backward(ctx, g_r, g_n):
+        r, row_norm, keep = ctx.saved_tensors
+        n, d = r.shape
+        if g_r is None and g_n is None:
+            return None, None, None, None, None
+        ldr = ldn = 0
+        if g_r is not None:
+            g_r, ldr = _rows(g_r)
+        if g_n is not None:
+            g_n, ldn = _rows(g_n)
+        dz = torch.empty_like(r)
+        L.call('igr_layer_tail_bwd_f32', n, d, _p(g_n), ldn, _p(g_r), ldr, _p(r), _p(row_norm), _p(keep),
+               ctx.consts[0], ctx.consts[1], _p(dz), _stream())
+        return dz, dz, None, None, None
+
+
+def layer_tail(a, b, p=0.0, training=False, slope=0.2):
+    """(r, F.normalize(r)) with r = F.dropout(F.leaky_relu(a + b, slope), p, training)
+    (model.py:4040-4042).  The dropout mask is one Bernoulli(1 - p) draw per element from
+    torch's generator of the device."""
+    keep, scale = None, 1.0
+    if training and p > 0:
+        keep = torch.empty(a.shape, dtype=torch.float32, device=a.device).bernoulli_(1.0 - p)
+        scale = 1.0 / (1.0 - p)
+    return LayerTail.apply(a, b, keep, scale, slope)
+
+
 class Propagate(torch.autograd.Function):
     """rep = mean_l(x_l), x_{l+1} = A x_l, x_0 = F emb (inductive) or emb.
 

@@ -1209,3 +1209,52 @@ def test_random_shapes_and_schedules_match_oracle(seed):
     for j in range(h):
         ref = O.spmm64(O.CSR(n_rows, n_cols, A.row_ptr, A.col, np.ascontiguousarray(r_csr[:, j])), k)
         close(yh[:, j * da:(j + 1) * da], ref, atol_row=2e-6)
+
+
+@pytest.mark.parametrize('d', [32, 64, 100, 128, 256])
+@pytest.mark.parametrize('drop', [False, True])
+def test_layer_tail_matches_torch(d, drop):
+    """r = dropout(leaky_relu(a + b, 0.2)), nrm = F.normalize(r) (model.py:4040-4042) in one
+    kernel each way against the torch float64 expression with the same mask: both outputs,
+    the gradient from both outputs (the normalised one arriving as a column block of a wider
+    gradient), from one of them alone, and an all-zero row (the norm's clamp)."""
+    n = 1003
+    rng = np.random.default_rng(d)
+    a = rng.standard_normal((n, d)).astype(np.float32)
+    b = rng.standard_normal((n, d)).astype(np.float32)
+    a[7], b[7] = 0., 0.
+    keep = (rng.random((n, d)) > 0.3).astype(np.float32) if drop else None
+    scale = 1 / 0.7 if drop else 1.0
+    wide = rng.standard_normal((n, 3 * d)).astype(np.float32)
+    gr = rng.standard_normal((n, d)).astype(np.float32)
+
+    def ref(use_r, use_n):
+        a64 = torch.tensor(a, dtype=torch.float64, requires_grad=True)
+        b64 = torch.tensor(b, dtype=torch.float64, requires_grad=True)
+        r = torch.nn.functional.leaky_relu(a64 + b64, 0.2)
+        if drop:
+            r = r * torch.tensor(keep, dtype=torch.float64) * scale
+        nrm = torch.nn.functional.normalize(r, p=2, dim=1)
+        loss = 0.
+        if use_r:
+            loss = loss + (r * torch.tensor(gr, dtype=torch.float64)).sum()
+        if use_n:
+            loss = loss + (nrm * torch.tensor(wide[:, d:2 * d], dtype=torch.float64)).sum()
+        loss.backward()
+        return r.detach().numpy(), nrm.detach().numpy(), a64.grad.numpy(), b64.grad.numpy()
+
+    for use_r, use_n in [(True, True), (False, True), (True, False)]:
+        at, bt = t(a).requires_grad_(True), t(b).requires_grad_(True)
+        r, nrm = ops.LayerTail.apply(at, bt, None if keep is None else t(keep), scale, 0.2)
+        loss = 0.
+        if use_r:
+            loss = loss + (r * t(gr)).sum()
+        if use_n:
+            loss = loss + (torch.cat([r.detach(), nrm, r.detach()], 1) * t(wide)).sum()
+        loss.backward()
+        r64, n64, ga, gb = ref(use_r, use_n)
+        close(r.detach().cpu().numpy(), r64, rtol=1e-6)
+        close(nrm.detach().cpu().numpy(), n64, rtol=2e-6, atol_row=1e-7)
+        close(at.grad.cpu().numpy(), ga, rtol=2e-5, atol_row=2e-6)
+        assert torch.equal(at.grad, bt.grad)
+    assert np.all(nrm.detach().cpu().numpy()[7] == 0)

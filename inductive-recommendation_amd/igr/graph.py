@@ -214,6 +214,23 @@ class Graph:
         g.values = values
         return g
 
+    def positional(self):
+        """This graph reading per-edge arrays by CSR position instead of by edge id (a view:
+        a caller that has permuted its values once, `values[g.edge_id]`, then reads them in
+        stream order in every product over this graph)."""
+        if self.edge_id is None:
+            return self
+        v = self.__dict__.get('_positional')
+        if v is None:
+            v = copy.copy(self)
+            v._base = getattr(self, '_base', None) or self
+            v.edge_id = None
+            v.csr = L.IgrCsr.from_buffer_copy(self.csr)
+            v.csr.edge_id = None
+            v._reverse = None
+            self._positional = v
+        return v
+
     def reverse(self):
         """Reverse graph for gspmm backward; its edge ids are this graph's edge ids."""
         base = getattr(self, '_base', None)

@@ -13,6 +13,7 @@ DGL-compatible surface (the reference's operator API):
     gsddmm(g, 'dot', lhs, rhs)                 ~ AttIGCN.masked_mm model.py:4246-4255
 """
 import ctypes
+import weakref
 import math
 
 import numpy as np
@@ -547,10 +548,28 @@ class GSpMMSum(torch.autograd.Function):
         dx = drhs = None
         dy = dy.contiguous()
         if ctx.needs_input_grad[1]:
-            dx = spmm(g.reverse(), dy, rhs)
+            rev = g.reverse()
+            if rhs is not None and rev.edge_id is not None and rhs.numel() == rev.nnz:
+                # the reverse graph reads the values through its edge ids; a model's layers share one
+                # value tensor, so permute it once and let every layer's product stream it in order
+                dx = spmm(rev.positional(), dy, _reverse_order_values(rev, rhs))
+            else:
+                dx = spmm(rev, dy, rhs)
         if ctx.needs_input_grad[2]:
             drhs = sddmm_dot(g, dy, x, 1).view(-1)
         return None, dx, drhs
+
+
+def _reverse_order_values(rev, vals):
+    """vals[rev.edge_id], kept for as long as `vals` itself is the tensor asked about (the cache
+    holds a weak reference and the tensor's version: another tensor, or this one after an
+    in-place write, is permuted afresh)."""
+    hit = rev.__dict__.get('_perm_cache')
+    if hit is not None and hit[0]() is vals and hit[1] == vals._version:
+        return hit[2]
+    perm = vals.detach()[rev.edge_id]
+    rev._perm_cache = (weakref.ref(vals), vals._version, perm)
+    return perm
 
 
 class GSDDMMDot(torch.autograd.Function):

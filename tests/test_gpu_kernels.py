@@ -1258,3 +1258,28 @@ def test_layer_tail_matches_torch(d, drop):
         close(at.grad.cpu().numpy(), ga, rtol=2e-5, atol_row=2e-6)
         assert torch.equal(at.grad, bt.grad)
     assert np.all(nrm.detach().cpu().numpy()[7] == 0)
+
+
+def test_gspmm_backward_streams_permuted_values():
+    """gspmm's backward permutes the edge values into the reverse graph's order once per value
+    tensor and streams them (Graph.positional): the same bits as reading them through the
+    edge ids - over two chained layers sharing the tensor, again after an in-place change of
+    the values, and for another value tensor."""
+    g, v = rand_graph(400, 400, 20000, seed=3, skew=True)
+    rev = g.reverse()
+    assert rev.edge_id is not None and rev.positional().edge_id is None
+    rng = np.random.default_rng(3)
+    dy = t(rng.standard_normal((400, 64)).astype(np.float32))
+
+    def check(values):
+        x = t(rng.standard_normal((400, 64)).astype(np.float32)).requires_grad_(True)
+        y2 = ops.gspmm(g, 'mul', 'sum', ops.gspmm(g, 'mul', 'sum', x, values), values)
+        (y2 * dy).sum().backward()
+        assert torch.equal(x.grad, ops.spmm(rev, ops.spmm(rev, dy, values), values))
+
+    vals = t(v)
+    check(vals)
+    check(vals)
+    vals.mul_(2.0)
+    check(vals)
+    check(t(rng.standard_normal(g.nnz).astype(np.float32)))

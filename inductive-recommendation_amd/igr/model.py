@@ -724,12 +724,15 @@ class IMCGAE(BasicModel):
 
     def get_rep(self):
         U, n = self.n_users, self.n_users + self.n_items
-        w = self.embedding.weight
-        x = w[:n]
-        ident, gen_u, gen_i = w[n], w[n + 1], w[n + 2]
-        s = torch.ones(n, 1, dtype=torch.float32, device=w.device)  # the repeated blocks' scalar per node
+        # tail rows: the identical vector, the users' general vector, the items' (one split: its
+        # backward is one concatenation, not a table-sized zero fill per selected row)
+        x, tail = torch.split(self.embedding.weight, [n, 3])
+        dev = x.device
+        # the repeated blocks' scalar per node, carried 32 wide (the narrowest width of the
+        # scheduled SpMM kernel; the any-width kernel gives a hub row to one lane); no gradient
+        s = torch.ones(n, 32, dtype=torch.float32, device=dev)
         acc = x
-        even, odd = s, torch.zeros_like(s)  # sums of s_l / (l + 1) over even / odd layers l
+        even, odd = s, None  # sums of s_l / (l + 1) over even / odd layers l
         for i in range(self.n_layers):
             mask = self.node_dropout_mask(i)
             if mask is not None:
@@ -737,21 +740,23 @@ class IMCGAE(BasicModel):
                 s = s * mask[:, None]
             x = ops.gspmm(self.norm_adj, 'mul', 'sum', x, self.norm_vals)
             with torch.no_grad():
-                # one scalar per node, carried 32 wide: the narrowest width of the scheduled SpMM
-                # kernel (the any-width kernel gives a row to one wave, a hub row to one lane)
-                s = ops.gspmm(self.norm_adj, 'mul', 'sum', s.expand(-1, 32).contiguous(), self.norm_vals)[:, :1]
-            acc = acc + x / float(i + 2)
-            if i % 2 == 0:
-                odd = odd + s / float(i + 2)  # layer i + 1
+                s = ops.gspmm(self.norm_adj, 'mul', 'sum', s, self.norm_vals)
+            inv = 1. / float(i + 2)
+            acc = torch.add(acc, x, alpha=inv)
+            if i % 2 == 0:  # layer i + 1 is odd
+                odd = s * inv if odd is None else torch.add(odd, s, alpha=inv)
             else:
-                even = even + s / float(i + 2)
-        # a user's general block: its own side's vector on even layers, the items' on odd ones
-        side = torch.zeros(n, 1, dtype=torch.float32, device=w.device)
-        side[:U] = 1.
-        own = side * gen_u[None, :] + (1. - side) * gen_i[None, :]
-        other = side * gen_i[None, :] + (1. - side) * gen_u[None, :]
-        general = even * own + odd * other
-        identical = (even + odd) * ident[None, :]
+                even = torch.add(even, s, alpha=inv)
+        # a user's general block: its own side's vector on even layers, the items' on odd ones.
+        # Per node the coefficients of (identical, users' general, items' general):
+        is_user = self.__dict__.get('_is_user')
+        if is_user is None or is_user.shape[0] != n or is_user.device != dev:
+            is_user = self._is_user = (torch.arange(n, device=dev) < U)[:, None]
+        e = even[:, :1]
+        o = torch.zeros_like(e) if odd is None else odd[:, :1]
+        coef = torch.cat([e + o, torch.where(is_user, e, o), torch.where(is_user, o, e)], dim=1)
+        general = ops.coef_product(coef[:, 1:], tail[1:])
+        identical = ops.coef_product(coef[:, :1], tail[:1])
         return torch.cat([acc, general, identical], dim=1)
 
     def bpr_forward(self, users, pos_items, neg_items):

@@ -494,7 +494,8 @@ def topk(scores, k, values=True):
 def gemm(a, b, bias=None, trans_a=False, trans_b=False):
     """C = A(m,k) B(k,n) + bias; b is [n, k] (Linear weight) unless trans_b."""
     _dev(a, b, bias)
-    a, b = _f32(a).contiguous(), _f32(b).contiguous()
+    a, _ = _rows(a)  # rows may be strided (a column block of a wider matrix)
+    b, _ = _rows(b)
     m, k = (a.shape[1], a.shape[0]) if trans_a else a.shape
     n = b.shape[1] if trans_b else b.shape[0]
     kb = b.shape[0] if trans_b else b.shape[1]
@@ -725,6 +726,26 @@ def linear(x, layer):
 
 def gather(src, idx, offset=0):
     return GatherRows.apply(src, idx, int(offset))
+
+
+class CoefProduct(torch.autograd.Function):
+    """coef @ b for per-row coefficients that take no gradient (coef [n, k], k small; b [k, d]):
+    the gradient of b is coef^T g, a k x d result reduced over all n rows - the split-K GEMM
+    (summed in a fixed order) instead of a one-workgroup library kernel."""
+
+    @staticmethod
+    def forward(ctx, coef, b):
+        ctx.save_for_backward(coef)
+        return gemm(coef, b, trans_b=True)
+
+    @staticmethod
+    def backward(ctx, g):
+        coef, = ctx.saved_tensors
+        return None, gemm(coef, g, trans_a=True, trans_b=True)
+
+
+def coef_product(coef, b):
+    return CoefProduct.apply(coef.detach(), b)
 
 
 LAYER_TAIL_MAX_WIDTH = 256

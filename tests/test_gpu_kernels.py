@@ -1283,3 +1283,24 @@ def test_gspmm_backward_streams_permuted_values():
     vals.mul_(2.0)
     check(vals)
     check(t(rng.standard_normal(g.nnz).astype(np.float32)))
+
+
+@pytest.mark.parametrize('n,k,d', [(9746, 2, 64), (9746, 1, 64), (70001, 3, 128), (5, 2, 32)])
+def test_coef_product_and_its_gradient(n, k, d):
+    """out = coef @ b with gradient-free per-row coefficients (IMCGAE's repeated blocks): the
+    product and d b = coef^T g (the split-K GEMM over all rows, g a column block of a wider
+    gradient) against float64; the same bits twice."""
+    rng = np.random.default_rng(n + k)
+    coef = rng.standard_normal((n, k)).astype(np.float32)
+    b = rng.standard_normal((k, d)).astype(np.float32)
+    wide = rng.standard_normal((n, 2 * d)).astype(np.float32)
+    grads = []
+    for _ in range(2):
+        bt = t(b).requires_grad_(True)
+        out = ops.coef_product(t(coef), bt)
+        (torch.cat([out, out.detach()], 1) * t(wide)).sum().backward()
+        grads.append(bt.grad)
+    close(out.detach().cpu().numpy(), coef.astype(np.float64) @ b.astype(np.float64), atol_row=2e-6)
+    ref = coef.astype(np.float64).T @ wide[:, :d].astype(np.float64)
+    assert np.abs(grads[0].cpu().numpy() - ref).max() <= 4e-6 * np.sqrt(n) * 4
+    assert torch.equal(grads[0], grads[1])

@@ -199,13 +199,17 @@ class LightGCN(BasicModel):
             rep_b = ops.propagate_rows(self.norm_adj, self.embedding.weight, self.n_layers, rows,
                                        adj_vals=self.norm_vals)
             bpr, _ = ops.bpr_loss(rep_b, iu, ip, ineg, 0, 0, distinct=True)
+            keys = None
         else:
             rep = self.get_rep()
             self._join_batch_stream(users, pos_items, neg_items)
-            bpr, _ = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users)
+            # both terms scatter their gradients over the same table rows: one sort serves both
+            keys = ops.rowsort(users, 0, pos_items, self.n_users, neg_items, self.n_users) \
+                if need_l2 and torch.is_grad_enabled() else None
+            bpr, _ = ops.bpr_loss(rep, users, pos_items, neg_items, 0, self.n_users, keys=keys)
         if not need_l2:
             return bpr, None
-        _, l2 = ops.bpr_loss(self.embedding.weight, users, pos_items, neg_items, 0, self.n_users)
+        _, l2 = ops.bpr_loss(self.embedding.weight, users, pos_items, neg_items, 0, self.n_users, keys=keys)
         return bpr, l2
 
 

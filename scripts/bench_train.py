@@ -31,6 +31,7 @@ def main():
     ap.add_argument('--batch-rep', default='auto', choices=['auto', 'true', 'false'],
                     help='last layer only at the batch rows (model.batch_rep_pays)')
     ap.add_argument('--model', default='IGCN', choices=['IGCN', 'AttIGCN', 'LightGCN', 'NGCF', 'IMCGAE'])
+    ap.add_argument('--l2-reg', type=float, default=0., help='trainer l2_reg (0 skips the l2 term, as the IGCN configs do)')
     ap.add_argument('--eval', action='store_true', help='also time one full eval ranking (Recall@20 path)')
     ap.add_argument('--graph', action='store_true', help='replay one hipGraph-captured step (trainer.StepGraph)')
     ap.add_argument('--dist-backend', default='nccl', help="'nccl' (= RCCL); 'gloo' for rehearsals (host-staged)")
@@ -96,7 +97,7 @@ def main():
                                 'batch_rep': {'auto': 'auto', 'true': True, 'false': False}[args.batch_rep]})
     igcn = args.model in ('IGCN', 'AttIGCN')
     tr = T.get_trainer({'name': 'IGCNTrainer' if igcn else 'BPRTrainer', 'optimizer': 'Adam', 'lr': 1e-3,
-                        'l2_reg': 0., 'aux_reg': 0.01, 'device': dev, 'n_epochs': 1, 'batch_size': args.batch,
+                        'l2_reg': args.l2_reg, 'aux_reg': 0.01, 'device': dev, 'n_epochs': 1, 'batch_size': args.batch,
                         'test_batch_size': 512, 'topks': [20]}, ds, m)
     building.set()
     print(f'built in {time.time() - t0:.1f}s: adj nnz {m.norm_adj.nnz}' +

@@ -753,9 +753,10 @@ class IMCGAE(BasicModel):
                 even = torch.add(even, s, alpha=inv)
         # a user's general block: its own side's vector on even layers, the items' on odd ones.
         # Per node the coefficients of (identical, users' general, items' general):
-        is_user = self.__dict__.get('_is_user')
-        if is_user is None or is_user.shape[0] != n or is_user.device != dev:
-            is_user = self._is_user = (torch.arange(n, device=dev) < U)[:, None]
+        cached = self.__dict__.get('_is_user')
+        if cached is None or cached[0] != (U, n, dev):
+            cached = self._is_user = ((U, n, dev), (torch.arange(n, device=dev) < U)[:, None])
+        is_user = cached[1]
         e = even[:, :1]
         o = torch.zeros_like(e) if odd is None else odd[:, :1]
         coef = torch.cat([e + o, torch.where(is_user, e, o), torch.where(is_user, o, e)], dim=1)

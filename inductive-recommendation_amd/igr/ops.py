@@ -796,7 +796,9 @@ def layer_tail(a, b, p=0.0, training=False, slope=0.2):
     (model.py:4040-4042).  The dropout mask is one Bernoulli(1 - p) draw per element from
     torch's generator of the device."""
     keep, scale = None, 1.0
-    if training and p > 0:
+    if training and p >= 1:  # F.dropout(p=1): all zeros
+        keep, scale = torch.zeros(a.shape, dtype=torch.float32, device=a.device), 0.0
+    elif training and p > 0:
         keep = torch.empty(a.shape, dtype=torch.float32, device=a.device).bernoulli_(1.0 - p)
         scale = 1.0 / (1.0 - p)
     return LayerTail.apply(a, b, keep, scale, slope)

@@ -225,10 +225,13 @@ class NGCF(BasicModel):
         kaiming_uniform_(self.embedding.weight)
         self.n_layers = len(self.layer_sizes)
         self.layer_sizes.insert(0, self.embedding_size)
-        self.gc_layers = nn.ModuleList(
-            [init_one_layer(self.layer_sizes[i - 1], self.layer_sizes[i]) for i in range(1, self.n_layers + 1)])
-        self.bi_layers = nn.ModuleList(
-            [init_one_layer(self.layer_sizes[i - 1], self.layer_sizes[i]) for i in range(1, self.n_layers + 1)])
+        # layer by layer, the gc layer before the bi layer: the generator's draws land on the same
+        # weights as in the reference's constructor (model.py:3998-4002)
+        gc, bi = [], []
+        for i in range(1, self.n_layers + 1):
+            gc.append(init_one_layer(self.layer_sizes[i - 1], self.layer_sizes[i]))
+            bi.append(init_one_layer(self.layer_sizes[i - 1], self.layer_sizes[i]))
+        self.gc_layers, self.bi_layers = nn.ModuleList(gc), nn.ModuleList(bi)
         self.norm_adj = self.generate_graph(model_config['dataset'])
         self.to(device=self.device)
 

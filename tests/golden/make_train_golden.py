@@ -14,6 +14,7 @@ tests/golden/train_<shape>.npz (IGCN) and, with `lightgcn`, the reference
 LightGCN under BPRTrainer's loss to tests/golden/train_lgcn_<shape>.npz.
 Run: python tests/golden/make_train_golden.py [shape ...]
      python tests/golden/make_train_golden.py lightgcn [shape ...]
+     python tests/golden/make_train_golden.py ngcf [shape ...]   (-> train_ngcf_<shape>.npz)
 """
 import os
 import sys
@@ -213,11 +214,69 @@ def run_lightgcn(shape, l2_reg=1e-4):
                         epochs=epochs, d=d, n_layers=L, l2_reg=l2_reg)
 
 
+def run_ngcf(shape, l2_reg=1e-3, epochs=6):
+    """The reference NGCF (model.py:3986-4055, config row 4: layer_sizes [d, d, d], l2_reg 1e-3)
+    under BPRTrainer's loss (trainer.py:412-429) on the same fixed batches, dropout 0 (the
+    edge mask and F.dropout are then the identity, so no random draw separates the runs)."""
+    install_stubs()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import model as ref_model
+    import trainer as ref_trainer
+    nu, ni, mean_deg, d, L, _ = ml_like.SHAPES[shape]
+    train, val, test = ml_like.splits_for(shape)
+    ds = DS(shape, nu, ni, train, val, test)
+    bs = 2048
+    spe = ml_like.steps_per_epoch(train, bs)
+    main_b = ml_like.batches_for(shape, train, ni, bs, spe * epochs, seed=1)
+    torch.manual_seed(13)
+    m = ref_model.NGCF({'name': 'NGCF', 'embedding_size': d, 'layer_sizes': [d, d, d], 'device': 'cpu',
+                        'dropout': 0., 'dataset': ds})
+    init = {k: (float(v.detach().double().sum()), float(v.detach().double().abs().sum()))
+            for k, v in m.named_parameters()}
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    tr = ref_trainer.BasicTrainer({'name': 'BasicTrainer', 'dataset': ds, 'model': m, 'topks': [1, 5, 10, 15, 20],
+                                   'device': 'cpu', 'n_epochs': 0, 'test_batch_size': 512})
+    losses, val_rec, test_rec, step_loss = [], [], [], []
+    t0 = time.time()
+    for ep in range(epochs):
+        m.train()
+        tot = 0.
+        for s in range(spe):
+            u, p, n = (torch.from_numpy(a) for a in main_b[ep * spe + s])
+            users_r, pos_items_r, neg_items_r, l2_norm_sq = m.bpr_forward(u, p, n)
+            pos_scores = torch.sum(users_r * pos_items_r, dim=1)
+            neg_scores = torch.sum(users_r * neg_items_r, dim=1)
+            loss = F.softplus(neg_scores - pos_scores).mean() + l2_reg * l2_norm_sq.mean()
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            tot += loss.item()
+            if ep == 0 and s < 20:
+                step_loss.append(loss.item())
+        losses.append(tot / spe)
+        _, met, _ = tr.eval('val')
+        val_rec.append(met['Recall'][20])
+        _, met, _ = tr.eval('test')
+        test_rec.append(met['Recall'][20])
+        print(f'ngcf {shape} epoch {ep}: loss {losses[-1]:.5f} val R@20 {val_rec[-1]:.4f} '
+              f'test R@20 {test_rec[-1]:.4f} ({time.time() - t0:.0f}s)', flush=True)
+    names = sorted(init)
+    np.savez_compressed(os.path.join(HERE, f'train_ngcf_{shape}.npz'), losses=np.array(losses),
+                        val_recall20=np.array(val_rec), test_recall20=np.array(test_rec),
+                        first_step_losses=np.array(step_loss), param_names=np.array(names),
+                        init_sum=np.array([init[k][0] for k in names]), init_abs=np.array([init[k][1] for k in names]),
+                        seed=13, epochs=epochs, d=d, l2_reg=l2_reg)
+
+
 if __name__ == '__main__':
     args = sys.argv[1:]
     if args and args[0] == 'lightgcn':
         for sh in (args[1:] or ['ml100k']):
             run_lightgcn(sh)
+    elif args and args[0] == 'ngcf':
+        for sh in (args[1:] or ['ml100k']):
+            run_ngcf(sh)
     else:
         for sh in (args or list(ml_like.SHAPES)):
             run(sh)

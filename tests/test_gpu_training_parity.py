@@ -157,6 +157,65 @@ def test_lightgcn_bpr_training_matches_reference(shape, batch_rep):
     np.testing.assert_allclose(first, ref['first_step_losses'], rtol=1e-4)
 
 
+@pytest.mark.parametrize('shape,fused', [('ml100k', True), ('ml100k', False), ('ml1m', True)])
+def test_ngcf_bpr_training_matches_reference(shape, fused):
+    """The reference NGCF (model.py:3986-4055, three d x d layer pairs as in config row 4)
+    under BPRTrainer's loss with l2_reg 1e-3 and dropout 0 (make_train_golden.py ngcf): igr
+    NGCF + BPRTrainer.step on the identical batches and initialisation - HIP SpMM, MFMA
+    Linear layers and their streamed weight gradients, the fused layer tail, and (fused) the
+    BPR terms on the rep rows with the fused Adam.  The first consecutive step losses (each
+    depends on every earlier update; 20 steps at the ML-100K shape, 10 at the ML-1M shape)
+    agree to 1e-5.  NGCF's trajectory is not stable beyond that: the reference run against
+    ITSELF with 8 CPU threads and with 1 (another summation order, nothing else) drifts to
+    1.5 % in the step loss within 19 steps at the ML-1M shape, and igr's fused and unfused
+    steps drift apart the same way.  So the epochs are held to what that instability leaves:
+    loss within 2 %, Recall@20 within 0.015."""
+    tight_steps = 20 if shape == 'ml100k' else 10
+    path = os.path.join(GOLDEN, f'train_ngcf_{shape}.npz')
+    if not os.path.exists(path):
+        pytest.skip(f'{path} not generated')
+    ref = np.load(path)
+    nu, ni, mean_deg, d, _, _ = ml_like.SHAPES[shape]
+    epochs = int(ref['epochs'])
+    train, val, test = ml_like.splits_for(shape)
+    ds = DS(shape, nu, ni, train, val, test)
+    bs = 2048
+    spe = ml_like.steps_per_epoch(train, bs)
+    main_b = ml_like.batches_for(shape, train, ni, bs, spe * epochs, seed=1)
+    torch.manual_seed(int(ref['seed']))
+    m = M.NGCF({'name': 'NGCF', 'embedding_size': d, 'layer_sizes': [d, d, d], 'device': DEV, 'dropout': 0.,
+                'dataset': ds})
+    params = dict(m.named_parameters())
+    for k, s_ref, a_ref in zip(ref['param_names'], ref['init_sum'], ref['init_abs']):
+        v = params[str(k)].detach().double()
+        assert float(v.sum()) == pytest.approx(float(s_ref), rel=1e-12, abs=1e-9), k
+        assert float(v.abs().sum()) == pytest.approx(float(a_ref), rel=1e-12, abs=1e-12), k
+    tr = T.get_trainer({'name': 'BPRTrainer', 'optimizer': 'Adam', 'lr': 1e-3, 'l2_reg': float(ref['l2_reg']),
+                        'device': DEV, 'n_epochs': epochs, 'batch_size': bs, 'test_batch_size': 512,
+                        'topks': [1, 5, 10, 15, 20], 'fused': fused}, ds, m)
+    t = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    first = []
+    for ep in range(epochs):
+        m.train()
+        tot = 0.
+        for s in range(spe):
+            u, p, n = main_b[ep * spe + s]
+            loss = float(tr.step(t(u), t(p), t(n)).detach())
+            tot += loss
+            if ep == 0 and s < 20:
+                first.append(loss)
+        _, vmet, _ = tr.eval('val')
+        _, tmet, _ = tr.eval('test')
+        if ep == 0:
+            np.testing.assert_allclose(first[:tight_steps], ref['first_step_losses'][:tight_steps], rtol=1e-5)
+        print(f'ngcf {shape} fused={fused} epoch {ep}: loss {tot / spe:.6f} (ref {float(ref["losses"][ep]):.6f}) '
+              f'val R@20 {vmet["Recall"][20]:.4f} ({float(ref["val_recall20"][ep]):.4f}) '
+              f'test R@20 {tmet["Recall"][20]:.4f} ({float(ref["test_recall20"][ep]):.4f})', flush=True)
+        np.testing.assert_allclose(tot / spe, ref['losses'][ep], rtol=2e-2)
+        assert abs(vmet['Recall'][20] - ref['val_recall20'][ep]) <= 0.015, (ep, vmet['Recall'][20])
+        assert abs(tmet['Recall'][20] - ref['test_recall20'][ep]) <= 0.015, (ep, tmet['Recall'][20])
+
+
 @pytest.mark.parametrize('shape', ['ml1m', 'ml1m_l3'])
 def test_production_path_recall_matches_reference(shape):
     """The DEFAULT training path - device BPR sampler, dropout drawn inside the SpMM

@@ -15,6 +15,7 @@ LightGCN under BPRTrainer's loss to tests/golden/train_lgcn_<shape>.npz.
 Run: python tests/golden/make_train_golden.py [shape ...]
      python tests/golden/make_train_golden.py lightgcn [shape ...]
      python tests/golden/make_train_golden.py ngcf [shape ...]   (-> train_ngcf_<shape>.npz)
+     python tests/golden/make_train_golden.py imcgae [shape ...] (-> train_imcgae_<shape>.npz)
 """
 import os
 import sys
@@ -269,6 +270,58 @@ def run_ngcf(shape, l2_reg=1e-3, epochs=6):
                         seed=13, epochs=epochs, d=d, l2_reg=l2_reg)
 
 
+def run_imcgae(shape, epochs=6):
+    """The reference IMCGAE (model.py:4300-4345, config row 7: 3 layers, dropout 0.3, l2_reg 0)
+    under BPRTrainer's loss on the same fixed batches; its node-dropout masks are the CPU
+    generator's draws (three F.dropout calls per step), which igr replays with
+    dropout_rng = 'cpu'."""
+    install_stubs()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import model as ref_model
+    import trainer as ref_trainer
+    nu, ni, mean_deg, d, _, _ = ml_like.SHAPES[shape]
+    train, val, test = ml_like.splits_for(shape)
+    ds = DS(shape, nu, ni, train, val, test)
+    bs = 2048
+    spe = ml_like.steps_per_epoch(train, bs)
+    main_b = ml_like.batches_for(shape, train, ni, bs, spe * epochs, seed=1)
+    torch.manual_seed(17)
+    m = ref_model.IMCGAE({'name': 'IMCGAE', 'embedding_size': d, 'n_layers': 3, 'device': 'cpu', 'dropout': 0.3,
+                          'dataset': ds})
+    e = m.embedding.weight.detach().double()
+    init_sum, init_abs = float(e.sum()), float(e.abs().sum())
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    tr = ref_trainer.BasicTrainer({'name': 'BasicTrainer', 'dataset': ds, 'model': m, 'topks': [1, 5, 10, 15, 20],
+                                   'device': 'cpu', 'n_epochs': 0, 'test_batch_size': 512})
+    losses, val_rec, test_rec, step_loss = [], [], [], []
+    t0 = time.time()
+    for ep in range(epochs):
+        m.train()
+        tot = 0.
+        for s in range(spe):
+            u, p, n = (torch.from_numpy(a) for a in main_b[ep * spe + s])
+            users_r, pos_items_r, neg_items_r, l2_norm_sq = m.bpr_forward(u, p, n)
+            loss = F.softplus(torch.sum(users_r * neg_items_r, dim=1) - torch.sum(users_r * pos_items_r, dim=1)).mean()
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            tot += loss.item()
+            if ep == 0 and s < 20:
+                step_loss.append(loss.item())
+        losses.append(tot / spe)
+        _, met, _ = tr.eval('val')
+        val_rec.append(met['Recall'][20])
+        _, met, _ = tr.eval('test')
+        test_rec.append(met['Recall'][20])
+        print(f'imcgae {shape} epoch {ep}: loss {losses[-1]:.5f} val R@20 {val_rec[-1]:.4f} '
+              f'test R@20 {test_rec[-1]:.4f} ({time.time() - t0:.0f}s)', flush=True)
+    np.savez_compressed(os.path.join(HERE, f'train_imcgae_{shape}.npz'), losses=np.array(losses),
+                        val_recall20=np.array(val_rec), test_recall20=np.array(test_rec),
+                        first_step_losses=np.array(step_loss), init_sum=init_sum, init_abs=init_abs, seed=17,
+                        epochs=epochs, d=d, n_layers=3, dropout=0.3)
+
+
 if __name__ == '__main__':
     args = sys.argv[1:]
     if args and args[0] == 'lightgcn':
@@ -277,6 +330,9 @@ if __name__ == '__main__':
     elif args and args[0] == 'ngcf':
         for sh in (args[1:] or ['ml100k']):
             run_ngcf(sh)
+    elif args and args[0] == 'imcgae':
+        for sh in (args[1:] or ['ml100k']):
+            run_imcgae(sh)
     else:
         for sh in (args or list(ml_like.SHAPES)):
             run(sh)

@@ -14,6 +14,7 @@ tests/golden/train_<shape>.npz (IGCN) and, with `lightgcn`, the reference
 LightGCN under BPRTrainer's loss to tests/golden/train_lgcn_<shape>.npz.
 Run: python tests/golden/make_train_golden.py [shape ...]
      python tests/golden/make_train_golden.py lightgcn [shape ...]
+     python tests/golden/make_train_golden.py imf [shape ...]    (-> train_imf_<shape>.npz)
      python tests/golden/make_train_golden.py ngcf [shape ...]   (-> train_ngcf_<shape>.npz)
      python tests/golden/make_train_golden.py imcgae [shape ...] (-> train_imcgae_<shape>.npz)
 """
@@ -97,12 +98,17 @@ class DS:
         return len(self.train_array)
 
 
-def run(shape):
+def run(shape, imf=False):
+    """imf: the reference's IMF (model.py:4290-4297; config row 6: the inductive layer alone,
+    dropout 0.1, l2_reg 1e-5, aux_reg 0.1) under the same IGCNTrainer loop, six epochs,
+    to train_imf_<shape>.npz."""
     install_stubs()
     sys.path.insert(0, REF)
     import model as ref_model
     import trainer as ref_trainer
     nu, ni, mean_deg, d, L, epochs = ml_like.SHAPES[shape]
+    if imf:
+        L, epochs = 0, 6
     train, val, test = ml_like.splits_for(shape)
     ds = DS(shape, nu, ni, train, val, test)
     bs = 2048
@@ -110,16 +116,16 @@ def run(shape):
     main_b = ml_like.batches_for(shape, train, ni, bs, spe * epochs, seed=1)
     aux_b = ml_like.batches_for(shape, train, ni, bs, spe * epochs, seed=2)  # feature_ratio = 1: aux maps are identity
     torch.manual_seed(7)
-    cfg = {'name': 'IGCN', 'embedding_size': d, 'n_layers': L, 'device': 'cpu', 'dropout': 0.3,
-           'feature_ratio': 1., 'dataset': ds}
-    m = ref_model.IGCN(cfg)
+    cfg = {'name': 'IMF' if imf else 'IGCN', 'embedding_size': d, 'n_layers': L, 'device': 'cpu',
+           'dropout': 0.1 if imf else 0.3, 'feature_ratio': 1., 'dataset': ds}
+    m = (ref_model.IMF if imf else ref_model.IGCN)(cfg)
     init_sum = float(m.embedding.weight.detach().double().sum())
     init_abs = float(m.embedding.weight.detach().double().abs().sum())
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     topks = [20]
     tr = ref_trainer.BasicTrainer({'name': 'BasicTrainer', 'dataset': ds, 'model': m, 'topks': [1, 5, 10, 15, 20],
                                    'device': 'cpu', 'n_epochs': 0, 'test_batch_size': 512})
-    l2_reg, aux_reg = 0., 0.01
+    l2_reg, aux_reg = (1.e-5, 0.1) if imf else (0., 0.01)
     losses, val_rec, val_ndcg, test_rec = [], [], [], []
     step_loss = []
     t0 = time.time()
@@ -157,7 +163,8 @@ def run(shape):
         test_rec.append(met['Recall'][20])
         print(f'{shape} epoch {ep}: loss {losses[-1]:.5f} val R@20 {val_rec[-1]:.4f} '
               f'test R@20 {test_rec[-1]:.4f} ({time.time() - t0:.0f}s)', flush=True)
-    np.savez_compressed(os.path.join(HERE, f'train_{shape}.npz'), losses=np.array(losses), val_recall20=np.array(val_rec),
+    np.savez_compressed(os.path.join(HERE, f'train_imf_{shape}.npz' if imf else f'train_{shape}.npz'),
+                        losses=np.array(losses), val_recall20=np.array(val_rec),
                         val_ndcg20=np.array(val_ndcg), test_recall20=np.array(test_rec),
                         first_step_losses=np.array(step_loss), init_sum=init_sum, init_abs=init_abs,
                         seed=7, epochs=epochs, d=d, n_layers=L, alpha_final=m.alpha)
@@ -327,6 +334,9 @@ if __name__ == '__main__':
     if args and args[0] == 'lightgcn':
         for sh in (args[1:] or ['ml100k']):
             run_lightgcn(sh)
+    elif args and args[0] == 'imf':
+        for sh in (args[1:] or ['ml100k']):
+            run(sh, imf=True)
     elif args and args[0] == 'ngcf':
         for sh in (args[1:] or ['ml100k']):
             run_ngcf(sh)

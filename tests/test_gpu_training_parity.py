@@ -101,6 +101,58 @@ def test_igcn_training_matches_reference(shape, batch_rep):
     assert m.alpha == pytest.approx(float(ref['alpha_final']))
 
 
+@pytest.mark.parametrize('shape', ['ml100k', 'ml1m'])
+def test_imf_training_matches_reference(shape):
+    """The reference's IMF (model.py:4290-4297; config row 6: the inductive layer alone,
+    dropout 0.1, l2_reg 1e-5, aux_reg 0.1) under IGCNTrainer's loop (make_train_golden.py imf):
+    igr IMF + IGCNTrainer.step with the reference's dropout draws on the identical batches and
+    initialisation - the l2 term over the rep rows included - reproduces the per-epoch losses
+    to 1e-5 and Recall@20 within 0.002 at every epoch."""
+    path = os.path.join(GOLDEN, f'train_imf_{shape}.npz')
+    if not os.path.exists(path):
+        pytest.skip(f'{path} not generated')
+    ref = np.load(path)
+    nu, ni, mean_deg, d, _, _ = ml_like.SHAPES[shape]
+    epochs = int(ref['epochs'])
+    train, val, test = ml_like.splits_for(shape)
+    ds = DS(shape, nu, ni, train, val, test)
+    bs = 2048
+    spe = ml_like.steps_per_epoch(train, bs)
+    main_b = ml_like.batches_for(shape, train, ni, bs, spe * epochs, seed=1)
+    aux_b = ml_like.batches_for(shape, train, ni, bs, spe * epochs, seed=2)
+    torch.manual_seed(int(ref['seed']))
+    m = M.IMF({'name': 'IMF', 'embedding_size': d, 'n_layers': 0, 'device': DEV, 'dropout': 0.1,
+               'feature_ratio': 1., 'dataset': ds, 'dropout_rng': 'cpu'})
+    e = m.embedding.weight.detach().double()
+    assert float(e.sum()) == pytest.approx(float(ref['init_sum']), rel=1e-12, abs=1e-9)
+    assert float(e.abs().sum()) == pytest.approx(float(ref['init_abs']), rel=1e-12)
+    tr = T.get_trainer({'name': 'IGCNTrainer', 'optimizer': 'Adam', 'lr': 1e-3, 'l2_reg': 1.e-5, 'aux_reg': 0.1,
+                        'device': DEV, 'n_epochs': epochs, 'batch_size': bs, 'test_batch_size': 512,
+                        'topks': [1, 5, 10, 15, 20]}, ds, m)
+    t = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    first = []
+    for ep in range(epochs):
+        m.train()
+        tot = 0.
+        for s in range(spe):
+            u, p, n = main_b[ep * spe + s]
+            au, ap, an = aux_b[ep * spe + s]
+            loss = float(tr.step(t(u), t(p), t(n), t(au), t(ap), t(an)).detach())
+            tot += loss
+            if ep == 0 and s < 20:
+                first.append(loss)
+        m.feat_mat_anneal()
+        _, vmet, _ = tr.eval('val')
+        _, tmet, _ = tr.eval('test')
+        print(f'imf {shape} epoch {ep}: loss {tot / spe:.6f} (ref {float(ref["losses"][ep]):.6f}) '
+              f'val R@20 {vmet["Recall"][20]:.4f} ({float(ref["val_recall20"][ep]):.4f})', flush=True)
+        np.testing.assert_allclose(tot / spe, ref['losses'][ep], rtol=1e-5)
+        assert abs(vmet['Recall'][20] - ref['val_recall20'][ep]) <= 0.002, (ep, vmet['Recall'][20])
+        assert abs(tmet['Recall'][20] - ref['test_recall20'][ep]) <= 0.002, (ep, tmet['Recall'][20])
+    np.testing.assert_allclose(first, ref['first_step_losses'], rtol=1e-5)
+    assert m.alpha == pytest.approx(float(ref['alpha_final']))
+
+
 @pytest.mark.parametrize('shape,batch_rep', [('ml100k', 'auto'), ('ml1m', 'auto'), ('ml100k', True)])
 def test_lightgcn_bpr_training_matches_reference(shape, batch_rep):
     """The reference LightGCN under BPRTrainer's loss (make_train_golden.py

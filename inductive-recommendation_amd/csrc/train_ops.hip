@@ -409,6 +409,94 @@ __global__ __launch_bounds__(256) void layer_tail_bwd_kernel(int64_t n, int d, c
     }
 }
 
+// The same two kernels for d = 4 LPR (d = 32, 64, 128, 256) with 16-byte aligned rows: LPR
+// lanes hold one row as float4s, 64 / LPR rows per wave, so every load and store instruction
+// moves whole 16-byte pieces (the one-float-per-lane form reads a 256-byte row with 64 lanes).
+typedef float tail_f4 __attribute__((ext_vector_type(4)));
+
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+    for (int m = LPR / 2; m >= 1; m >>= 1) v += shfl_xor_f(v, m);
+    return v;
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void layer_tail_vec_kernel(int64_t n, const float *__restrict__ a, int64_t lda,
+                                                             const float *__restrict__ b, int64_t ldb,
+                                                             const float *__restrict__ keep, float keep_scale,
+                                                             float slope, float *__restrict__ r,
+                                                             float *__restrict__ nrm, int64_t ldn,
+                                                             float *__restrict__ row_norm) {
+    constexpr int RPW = 64 / LPR, D = 4 * LPR;
+    const int lane = threadIdx.x & 63, sub = lane % LPR;
+    const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+    const bool live = row < n;
+    const int64_t rr = live ? row : n - 1;  // every lane stays for the shuffles; dead rows are not stored
+    const tail_f4 av = *reinterpret_cast<const tail_f4 *>(a + rr * lda + 4 * sub);
+    const tail_f4 bv = *reinterpret_cast<const tail_f4 *>(b + rr * ldb + 4 * sub);
+    tail_f4 y;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float z = av[q] + bv[q];
+        y[q] = z > 0.f ? z : z * slope;
+    }
+    if (keep) {
+        const tail_f4 kv = *reinterpret_cast<const tail_f4 *>(keep + rr * D + 4 * sub);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y[q] = y[q] * kv[q] * keep_scale;
+    }
+    const float ss = group_sum<LPR>(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
+    const float nr = fmaxf(sqrtf(ss), kNormEps);
+    if (!live) return;
+    *reinterpret_cast<tail_f4 *>(r + row * D + 4 * sub) = y;
+    *reinterpret_cast<tail_f4 *>(nrm + row * ldn + 4 * sub) = tail_f4{y[0] / nr, y[1] / nr, y[2] / nr, y[3] / nr};
+    if (sub == 0) row_norm[row] = nr;
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void layer_tail_bwd_vec_kernel(int64_t n, const float *__restrict__ gn, int64_t ldgn,
+                                                                 const float *__restrict__ gr, int64_t ldgr,
+                                                                 const float *__restrict__ r,
+                                                                 const float *__restrict__ row_norm,
+                                                                 const float *__restrict__ keep, float keep_scale,
+                                                                 float slope, float *__restrict__ dz) {
+    constexpr int RPW = 64 / LPR, D = 4 * LPR;
+    const int lane = threadIdx.x & 63, sub = lane % LPR;
+    const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+    const bool live = row < n;
+    const int64_t rr = live ? row : n - 1;
+    const float nr = row_norm[rr];
+    const tail_f4 rv = *reinterpret_cast<const tail_f4 *>(r + rr * D + 4 * sub);
+    tail_f4 g = tail_f4{0.f, 0.f, 0.f, 0.f};
+    float dot = 0.f;
+    if (gn) {
+        g = *reinterpret_cast<const tail_f4 *>(gn + rr * ldgn + 4 * sub);
+        dot = g[0] * rv[0] + g[1] * rv[1] + g[2] * rv[2] + g[3] * rv[3];
+    }
+    dot = group_sum<LPR>(dot);
+    const float proj = nr > kNormEps ? dot / (nr * nr) : 0.f;
+    tail_f4 t = tail_f4{0.f, 0.f, 0.f, 0.f};
+    if (gn) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] = (g[q] - rv[q] * proj) / nr;
+    }
+    if (gr) {
+        const tail_f4 gv = *reinterpret_cast<const tail_f4 *>(gr + rr * ldgr + 4 * sub);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] += gv[q];
+    }
+    if (keep) {
+        const tail_f4 kv = *reinterpret_cast<const tail_f4 *>(keep + rr * D + 4 * sub);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] = t[q] * kv[q] * keep_scale;
+    }
+    if (!live) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = rv[q] > 0.f ? t[q] : t[q] * slope;
+    *reinterpret_cast<tail_f4 *>(dz + row * D + 4 * sub) = t;
+}
+
 }  // namespace igr
 
 static bool tail_args_ok(const char *fn, int64_t n, int32_t d) {
@@ -430,6 +518,19 @@ extern "C" int igr_layer_tail_f32(int64_t n, int32_t d, const float *a, int64_t 
         if (lda < d || ldb < d || ldn < d) return arg_error(fn, "leading dimension too small");
         if ((n + 3) / 4 > 2147483647) return arg_error(fn, "too many rows");
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        const bool vec = (d == 32 || d == 64 || d == 128 || d == 256) && lda % 4 == 0 && ldb % 4 == 0 &&
+                         ldn % 4 == 0 && aligned16(a) && aligned16(b) && aligned16(r) && aligned16(nrm) &&
+                         (!keep || aligned16(keep));
+        if (vec) {
+            const int64_t rows_per_block = 4 * (64 / (d / 4));
+            const dim3 gv((unsigned)((n + rows_per_block - 1) / rows_per_block));
+#define IGR_TAILV(L_)                                                                                              \
+    hipLaunchKernelGGL((layer_tail_vec_kernel<L_>), gv, dim3(256), 0, st, n, a, lda, b, ldb, keep, keep_scale, slope, r, \
+                       nrm, ldn, row_norm)
+            if (d == 32) IGR_TAILV(8); else if (d == 64) IGR_TAILV(16); else if (d == 128) IGR_TAILV(32); else IGR_TAILV(64);
+#undef IGR_TAILV
+            return launch_status(fn);
+        }
         const dim3 grid((unsigned)((n + 3) / 4));
 #define IGR_TAIL(V_)                                                                                             \
     hipLaunchKernelGGL((layer_tail_kernel<V_>), grid, dim3(256), 0, st, n, (int)d, a, lda, b, ldb, keep, keep_scale, \
@@ -451,6 +552,19 @@ extern "C" int igr_layer_tail_bwd_f32(int64_t n, int32_t d, const float *gn, int
         if ((gn && ldgn < d) || (gr && ldgr < d)) return arg_error(fn, "leading dimension too small");
         if ((n + 3) / 4 > 2147483647) return arg_error(fn, "too many rows");
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        const bool vec = (d == 32 || d == 64 || d == 128 || d == 256) && aligned16(r) && aligned16(dz) &&
+                         (!gn || (ldgn % 4 == 0 && aligned16(gn))) && (!gr || (ldgr % 4 == 0 && aligned16(gr))) &&
+                         (!keep || aligned16(keep));
+        if (vec) {
+            const int64_t rows_per_block = 4 * (64 / (d / 4));
+            const dim3 gv((unsigned)((n + rows_per_block - 1) / rows_per_block));
+#define IGR_TAILBV(L_)                                                                                             \
+    hipLaunchKernelGGL((layer_tail_bwd_vec_kernel<L_>), gv, dim3(256), 0, st, n, gn, ldgn, gr, ldgr, r, row_norm, keep, \
+                       keep_scale, slope, dz)
+            if (d == 32) IGR_TAILBV(8); else if (d == 64) IGR_TAILBV(16); else if (d == 128) IGR_TAILBV(32); else IGR_TAILBV(64);
+#undef IGR_TAILBV
+            return launch_status(fn);
+        }
         const dim3 grid((unsigned)((n + 3) / 4));
 #define IGR_TAILB(V_)                                                                                              \
     hipLaunchKernelGGL((layer_tail_bwd_kernel<V_>), grid, dim3(256), 0, st, n, (int)d, gn, ldgn, gr, ldgr, r, row_norm, \

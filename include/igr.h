@@ -488,6 +488,13 @@ int igr_adam_multi_f32(int32_t n_slots, const igr_adam_slot *slots, double lr, d
  * captured training step advances at its end). */
 int igr_counter_add(int64_t *counter, int64_t value, void *stream);
 
+/* One value per node: y[r] = sum_{p in row r} rhs[eid(p)] * x[col[p]] (rhs NULL = 1), x [n_cols],
+ * y [n_rows].  The width-1 case of gspmm(g, 'mul', 'sum', x, rhs) (reference model.py:4335 for
+ * IMCGAE's repeated blocks, which stay one scalar per node through every layer).  Uses the
+ * graph's row schedule when it has one (hub rows take a workgroup each); fixed summation
+ * order. */
+int igr_spmv_f32(const igr_csr *g, const float *x, const float *rhs, float *y, void *stream);
+
 /* NGCF layer tail (reference model.py:4040-4042, after the two Linear layers):
  *   r   = dropout(leaky_relu(a + b, slope))     keep: 0/1 per element ([n, d], NULL = no
  *                                               dropout), kept elements times keep_scale

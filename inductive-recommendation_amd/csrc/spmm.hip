@@ -790,3 +790,84 @@ extern "C" int igr_edge_dropout_counter_f32(const igr_csr *g, const float *val, 
         return launch_status(fn);
     });
 }
+
+// ---------------------------------------------------------------------------
+// igr_spmv_f32: y[r] = sum_{p in row r} w(p) x[col[p]] for ONE value per node (IMCGAE's two
+// repeated blocks stay rank one through every layer, model.py:4326-4337, so they follow from
+// one scalar per node and layer).  4 bytes gathered per edge from a vector that fits L2, so
+// the work is the streamed CSR: 16 lanes share a row (lane l takes edges l, l + 16, ...; a
+// fixed xor tree adds the 16 partial sums), rows the schedule split (hub rows) take a whole
+// workgroup each.  Fixed summation orders: the same bits on every run.
+namespace igr {
+
+__global__ __launch_bounds__(256) void spmv_rows_kernel(int64_t n_list, const int32_t *__restrict__ list,
+                                                        const int64_t *__restrict__ row_ptr,
+                                                        const int32_t *__restrict__ col,
+                                                        const int64_t *__restrict__ eid,
+                                                        const float *__restrict__ rhs, const float *__restrict__ x,
+                                                        float *__restrict__ y) {
+    const int64_t grp = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    if (grp >= n_list) return;  // whole 16-lane groups leave together; the shuffles stay inside a group
+    const int l = threadIdx.x & 15;
+    const int64_t r = list ? list[grp] : grp;
+    const int64_t beg = row_ptr[r], end = row_ptr[r + 1];
+    float s = 0.f;
+    for (int64_t p = beg + l; p < end; p += 16) {
+        const float w = rhs ? rhs[eid ? eid[p] : p] : 1.f;
+        s += w * x[col[p]];
+    }
+    s += shfl_xor_f(s, 8);
+    s += shfl_xor_f(s, 4);
+    s += shfl_xor_f(s, 2);
+    s += shfl_xor_f(s, 1);
+    if (l == 0) y[r] = s;
+}
+
+__global__ __launch_bounds__(256) void spmv_split_kernel(const int32_t *__restrict__ split_row,
+                                                         const int64_t *__restrict__ row_ptr,
+                                                         const int32_t *__restrict__ col,
+                                                         const int64_t *__restrict__ eid,
+                                                         const float *__restrict__ rhs, const float *__restrict__ x,
+                                                         float *__restrict__ y) {
+    __shared__ float part[256];
+    const int t = threadIdx.x;
+    const int64_t r = split_row[blockIdx.x];
+    const int64_t beg = row_ptr[r], end = row_ptr[r + 1];
+    float s = 0.f;
+    for (int64_t p = beg + t; p < end; p += 256) {
+        const float w = rhs ? rhs[eid ? eid[p] : p] : 1.f;
+        s += w * x[col[p]];
+    }
+    part[t] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) part[t] += part[t + o];
+        __syncthreads();
+    }
+    if (t == 0) y[r] = part[0];
+}
+
+}  // namespace igr
+
+extern "C" int igr_spmv_f32(const igr_csr *g, const float *x, const float *rhs, float *y, void *stream) {
+    return guarded("igr_spmv_f32", [&]() -> int {
+        const char *fn = "igr_spmv_f32";
+        if (!g) return arg_error(fn, "graph is NULL");
+        if (g->n_rows <= 0) return IGR_OK;
+        if (!y || !g->row_ptr || (g->nnz > 0 && (!x || !g->col_idx))) return arg_error(fn, "NULL pointer");
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        // the schedule's two lists cover every row once: unsplit rows (16 lanes each), split rows
+        // (a workgroup each); without a schedule every row takes 16 lanes
+        const bool planned = g->order && g->n_order > 0 && g->n_order + g->n_split == g->n_rows &&
+                             (g->n_split == 0 || g->split_row) && g->n_split <= 2147483647;
+        const int64_t n_list = planned ? g->n_order : g->n_rows;
+        const int64_t blocks = (n_list * 16 + 255) / 256;
+        if (blocks > 2147483647) return arg_error(fn, "too many rows");
+        hipLaunchKernelGGL(spmv_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n_list,
+                           planned ? g->order : nullptr, g->row_ptr, g->col_idx, g->edge_id, rhs, x, y);
+        if (planned && g->n_split > 0)
+            hipLaunchKernelGGL(spmv_split_kernel, dim3((unsigned)g->n_split), dim3(256), 0, st, g->split_row,
+                               g->row_ptr, g->col_idx, g->edge_id, rhs, x, y);
+        return launch_status(fn);
+    });
+}

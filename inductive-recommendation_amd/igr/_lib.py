@@ -115,6 +115,7 @@ SIGNATURES = {
     'igr_adam_multi_f32': (ctypes.c_int, [c_i32, c_vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                           ctypes.c_double, ctypes.c_double, c_vp, c_vp]),
     'igr_counter_add': (ctypes.c_int, [c_vp, c_i64, c_vp]),
+    'igr_spmv_f32': (ctypes.c_int, [_P(IgrCsr), c_vp, c_vp, c_vp, c_vp]),
     'igr_layer_tail_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, ctypes.c_float, ctypes.c_float,
                                           c_vp, c_vp, c_i64, c_vp, c_vp]),
     'igr_layer_tail_bwd_f32': (ctypes.c_int, [c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, ctypes.c_float,

@@ -735,19 +735,18 @@ class IMCGAE(BasicModel):
         # backward is one concatenation, not a table-sized zero fill per selected row)
         x, tail = torch.split(self.embedding.weight, [n, 3])
         dev = x.device
-        # the repeated blocks' scalar per node, carried 32 wide (the narrowest width of the
-        # scheduled SpMM kernel; the any-width kernel gives a hub row to one lane); no gradient
-        s = torch.ones(n, 32, dtype=torch.float32, device=dev)
+        # the repeated blocks' scalar per node (a width-1 product per layer, ops.spmv); no gradient
+        s = torch.ones(n, dtype=torch.float32, device=dev)
         acc = x
         even, odd = s, None  # sums of s_l / (l + 1) over even / odd layers l
         for i in range(self.n_layers):
             mask = self.node_dropout_mask(i)
             if mask is not None:
                 x = x * mask[:, None]
-                s = s * mask[:, None]
+                s = s * mask
             x = ops.gspmm(self.norm_adj, 'mul', 'sum', x, self.norm_vals)
             with torch.no_grad():
-                s = ops.gspmm(self.norm_adj, 'mul', 'sum', s, self.norm_vals)
+                s = ops.spmv(self.norm_adj, s, self.norm_vals)
             inv = 1. / float(i + 2)
             acc = torch.add(acc, x, alpha=inv)
             if i % 2 == 0:  # layer i + 1 is odd
@@ -760,8 +759,8 @@ class IMCGAE(BasicModel):
         if cached is None or cached[0] != (U, n, dev):
             cached = self._is_user = ((U, n, dev), (torch.arange(n, device=dev) < U)[:, None])
         is_user = cached[1]
-        e = even[:, :1]
-        o = torch.zeros_like(e) if odd is None else odd[:, :1]
+        e = even[:, None]
+        o = torch.zeros_like(e) if odd is None else odd[:, None]
         coef = torch.cat([e + o, torch.where(is_user, e, o), torch.where(is_user, o, e)], dim=1)
         general = ops.coef_product(coef[:, 1:], tail[1:])
         identical = ops.coef_product(coef[:, :1], tail[:1])

@@ -114,6 +114,22 @@ def spmm(g: Graph, x, rhs=None, out=None, epi=None):
     return out
 
 
+def spmv(g: Graph, x, rhs=None):
+    """y[r] = sum_{p in row r} rhs[eid(p)] x[col[p]]: one value per node (igr_spmv_f32), the
+    width-1 gspmm 'mul'/'sum'.  No gradient."""
+    _dev(x, rhs)
+    x = _f32(x).contiguous().view(-1)
+    if x.numel() < g.n_cols:
+        raise IgrError(f'spmv: x has {x.numel()} values, graph has {g.n_cols} source nodes')
+    if rhs is not None:
+        rhs = _f32(rhs).contiguous()
+        if rhs.numel() != g.nnz:
+            raise IgrError(f'rhs has {rhs.numel()} values, graph has {g.nnz} edges')
+    y = torch.empty(g.n_rows, dtype=torch.float32, device=x.device)
+    L.call('igr_spmv_f32', ctypes.byref(g.csr), _p(x), _p(rhs), _p(y), _stream())
+    return y
+
+
 # Widths the scheduled SpMM kernel is built for.  Any other width goes through it too, in
 # column blocks of these widths with the last one zero-padded: the any-width kernel of the
 # library gives a row to one wave and a feature to one lane, so a hub row at width 1 is one

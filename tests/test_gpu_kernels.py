@@ -1175,6 +1175,11 @@ def test_random_shapes_and_schedules_match_oracle(seed):
     ref = O.spmm64(A, x)
     bound = 1e-5 * np.abs(ref) + 2e-6 * max(np.abs(ref).max(initial=0.), 1e-30)  # tensor scale: d may be 1
     assert np.all(np.abs(y - ref) <= bound)
+    # one value per node (the width-1 product)
+    yv = ops.spmv(g, t(np.ascontiguousarray(x[:, 0])), t(v)).cpu().numpy()
+    ref1 = O.spmm64(A, np.ascontiguousarray(x[:, :1]))[:, 0]
+    mag = O.spmm64(O.CSR(n_rows, n_cols, A.row_ptr, A.col, np.abs(A.val)), np.abs(x[:, :1]))[:, 0]
+    assert np.all(np.abs(yv - ref1) <= 2e-6 * mag + 1e-30)
     # the transposed product, as the backward takes it: the reverse graph reads values by edge id
     r = g.reverse()
     gy = rng.standard_normal((n_rows, d)).astype(np.float32)
@@ -1304,3 +1309,26 @@ def test_coef_product_and_its_gradient(n, k, d):
     ref = coef.astype(np.float64).T @ wide[:, :d].astype(np.float64)
     assert np.abs(grads[0].cpu().numpy() - ref).max() <= 4e-6 * np.sqrt(n) * 4
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize('dedup', [True, False])
+def test_spmv_matches_oracle(dedup):
+    """y[r] = sum_p rhs[eid(p)] x[col[p]] (one value per node): hub rows through the schedule's
+    split list, unsplit and empty rows, duplicate edges read by edge id, unit weights, a graph
+    without a schedule; the same bits twice."""
+    for kw in (dict(split_threshold=32, chunk_edges=64), dict(split_threshold=1 << 30, chunk_edges=64), {}):
+        g, v = rand_graph(900, 5000, 40000, seed=41, skew=True, dedup=dedup, **kw)
+        if kw.get('split_threshold') == 32:
+            assert g.n_split > 20 and g.n_order + g.n_split == g.n_rows
+        x = np.random.default_rng(2).standard_normal(5000).astype(np.float32)
+        A = oracle_csr(g, v)
+        mag = O.spmm64(O.CSR(900, 5000, A.row_ptr, A.col, np.abs(A.val)), np.abs(x)[:, None])[:, 0]
+        y = ops.spmv(g, t(x), t(v))
+        assert np.all(np.abs(y.cpu().numpy() - O.spmm64(A, x[:, None])[:, 0]) <= 2e-6 * mag + 1e-30)
+        assert torch.equal(y, ops.spmv(g, t(x), t(v)))
+        A.val = np.ones_like(A.val)
+        y1 = ops.spmv(g, t(x)).cpu().numpy()
+        mag1 = O.spmm64(A, np.abs(x)[:, None])[:, 0]
+        assert np.all(np.abs(y1 - O.spmm64(A, x[:, None])[:, 0]) <= 2e-6 * mag1 + 1e-30)
+        empty = np.diff(g.host()['row_ptr']) == 0
+        assert empty.any() and np.all(y1[empty] == 0)

@@ -94,6 +94,8 @@ def spmm(g: Graph, x, rhs=None, out=None, epi=None):
         if rhs.numel() != g.nnz:
             raise IgrError(f'rhs has {rhs.numel()} values, graph has {g.nnz} edges')
         rhs = rhs.contiguous()
+    if out is None and epi is None and d == 1 and g.nnz and g.n_rows:
+        return spmv(g, x[:, 0], rhs).view(-1, 1)  # one value per node: the streamed-CSR kernel
     if out is None and epi is None and d not in _SCHEDULED_WIDTHS and g.nnz and g.n_rows:
         return _spmm_other_width(g, x, rhs, d)
     if out is None:

@@ -227,6 +227,9 @@ def test_new_entry_points_validate_arguments():
     _refused('igr_adam_f32', 4, F, F, F, F, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None, st, match='step')
     _refused('igr_bpr_sample', 4, 0, F, F, F, 10, 1, 0, None, 8, F, F, F, st, match='active')
     _refused('igr_spmm_heads_f32', ctypes.byref(rect.csr), 4, 64, F, 64, F, F, 256, None, st, match='leading')
+    # one value per node: graph and pointers
+    _refused('igr_spmv_f32', None, F, None, F, st, match='NULL')
+    _refused('igr_spmv_f32', ctypes.byref(rect.csr), F, None, None, st, match='NULL')
     # NGCF's layer tail: width and leading dimensions
     _refused('igr_layer_tail_f32', 4, 300, F, 300, F, 300, None, 1.0, 0.2, F, F, 300, F, st, match='d <= 256')
     _refused('igr_layer_tail_f32', 4, 64, F, 32, F, 64, None, 1.0, 0.2, F, F, 64, F, st, match='leading')

@@ -839,6 +839,17 @@ def test_empty_graphs_and_odd_widths():
     assert w.numel() == 0
     gn, _ = rand_graph(0, 7, 0, seed=2)
     assert ops.spmm(gn, x).shape == (0, 64)
+    # one value per node, the layer tail and the coefficient product on degenerate shapes
+    assert ops.spmv(g0, x[:, 0].contiguous()).abs().max().item() == 0
+    assert ops.spmv(gn, x[:, 0].contiguous()).shape == (0,)
+    assert ops.spmm(g0, x[:, :1].contiguous()).shape == (5, 1)
+    e = torch.zeros(0, 64, device=DEV)
+    r0, n0 = ops.layer_tail(e, e)
+    assert r0.shape == (0, 64) and n0.shape == (0, 64)
+    one = t(np.array([[3.0, -4.0, 0.0]], np.float32))  # a single row, width 3: the one-float-per-lane kernel
+    r1, n1 = ops.layer_tail(one, torch.zeros_like(one))
+    np.testing.assert_allclose(r1.cpu().numpy(), [[3.0, -0.8, 0.0]], rtol=1e-6)
+    np.testing.assert_allclose(n1.cpu().numpy(), np.array([[3.0, -0.8, 0.0]]) / np.sqrt(9.64), rtol=1e-6)
     g, v = rand_graph(60, 40, 900, seed=3)
     A = oracle_csr(g, v)
     for d in (3, 30, 66):

@@ -153,6 +153,16 @@ def test_reverse_graph_edge_ids():
     rrows = np.repeat(np.arange(30), np.diff(rh['row_ptr']))
     np.testing.assert_array_equal(src[rh['edge_id']], rrows)
     np.testing.assert_array_equal(dst[rh['edge_id']], rh['col_idx'])
+    # the positional view: same arrays, schedule and workspaces, per-edge data read by CSR position
+    p = r.positional()
+    assert p is r.positional() and p.edge_id is None and not p.csr.edge_id and r.csr.edge_id
+    assert p.csr.row_ptr == r.csr.row_ptr and p.csr.col_idx == r.csr.col_idx and p.csr.n_chunks == r.csr.n_chunks
+    assert p._ws is r._ws and p.reverse() is r.reverse()
+    # values permuted once (vals[edge_id]) then read in order = values read through the edge ids
+    vals = rng.standard_normal(400).astype(np.float32)
+    np.testing.assert_array_equal(vals[rh['edge_id']][np.arange(r.nnz)], vals[rh['edge_id']])
+    plain = ops.graph((torch.arange(5), torch.arange(5)), num_nodes=5, device='cpu')
+    assert plain.positional() is plain  # no edge-id permutation: the graph itself
 
 
 def _refused(name, *args, match=None):

@@ -580,14 +580,19 @@ class GSpMMSum(torch.autograd.Function):
 
 
 def _reverse_order_values(rev, vals):
-    """vals[rev.edge_id], kept for as long as `vals` itself is the tensor asked about (the cache
-    holds a weak reference and the tensor's version: another tensor, or this one after an
-    in-place write, is permuted afresh)."""
+    """vals[rev.edge_id], kept for as long as `vals` itself lives and is the tensor asked about
+    (the cache holds a weak reference and the tensor's version: another tensor, or this one
+    after an in-place write, is permuted afresh; when the tensor dies the copy is dropped)."""
     hit = rev.__dict__.get('_perm_cache')
     if hit is not None and hit[0]() is vals and hit[1] == vals._version:
         return hit[2]
     perm = vals.detach()[rev.edge_id]
-    rev._perm_cache = (weakref.ref(vals), vals._version, perm)
+
+    def forget(ref, rev=rev):  # the value tensor is gone: so is its permuted copy
+        held = rev.__dict__.get('_perm_cache')
+        if held is not None and held[0] is ref:
+            del rev.__dict__['_perm_cache']
+    rev._perm_cache = (weakref.ref(vals, forget), vals._version, perm)
     return perm
 
 

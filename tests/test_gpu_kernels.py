@@ -1343,3 +1343,25 @@ def test_spmv_matches_oracle(dedup):
         assert np.all(np.abs(y1 - O.spmm64(A, x[:, None])[:, 0]) <= 2e-6 * mag1 + 1e-30)
         empty = np.diff(g.host()['row_ptr']) == 0
         assert empty.any() and np.all(y1[empty] == 0)
+
+
+def test_gspmm_backward_permuted_copy_lives_with_its_values():
+    """The reverse-order copy of the edge values is dropped when the value tensor dies and kept
+    while it lives (a model's persistent values: one permutation for the whole training)."""
+    import gc
+    g, v = rand_graph(300, 300, 8000, seed=9, skew=True)
+    rev = g.reverse()
+    dy = t(np.random.default_rng(1).standard_normal((300, 32)).astype(np.float32))
+
+    def run(values):
+        x = t(np.random.default_rng(2).standard_normal((300, 32)).astype(np.float32)).requires_grad_(True)
+        (ops.gspmm(g, 'mul', 'sum', x, values) * dy).sum().backward()
+        return x.grad
+
+    keep = t(v)
+    g1 = run(keep)
+    held = rev.__dict__['_perm_cache'][2]
+    assert torch.equal(run(keep), g1) and rev.__dict__['_perm_cache'][2] is held  # reused, not redone
+    run(t(v) * 2)  # a temporary value tensor ...
+    gc.collect()
+    assert '_perm_cache' not in rev.__dict__  # ... takes its copy with it

@@ -30,7 +30,7 @@ def main():
     ap.add_argument('--batch', type=int, default=2048)
     ap.add_argument('--batch-rep', default='auto', choices=['auto', 'true', 'false'],
                     help='last layer only at the batch rows (model.batch_rep_pays)')
-    ap.add_argument('--model', default='IGCN', choices=['IGCN', 'AttIGCN', 'LightGCN', 'NGCF', 'IMCGAE'])
+    ap.add_argument('--model', default='IGCN', choices=['IGCN', 'AttIGCN', 'LightGCN', 'NGCF', 'IMCGAE', 'IMF'])
     ap.add_argument('--l2-reg', type=float, default=0., help='trainer l2_reg (0 skips the l2 term, as the IGCN configs do)')
     ap.add_argument('--eval', action='store_true', help='also time one full eval ranking (Recall@20 path)')
     ap.add_argument('--graph', action='store_true', help='replay one hipGraph-captured step (trainer.StepGraph)')
@@ -90,12 +90,14 @@ def main():
     t0 = time.time()
     if args.sharded:
         return sharded(args, ds, rank, world, dev)
+    if args.model == 'IMF':
+        args.layers = 0  # the inductive layer alone (model.py:4290-4297)
     m = getattr(M, args.model)({'name': args.model, 'embedding_size': args.d, 'n_layers': args.layers,
                                 'layer_sizes': [args.d] * args.layers,  # NGCF (config.py: [64, 64, 64])
                                 'device': dev, 'dropout': 0.3 if args.model != 'NGCF' else 0.1, 'feature_ratio': 1.,
                                 'dataset': ds,
                                 'batch_rep': {'auto': 'auto', 'true': True, 'false': False}[args.batch_rep]})
-    igcn = args.model in ('IGCN', 'AttIGCN')
+    igcn = args.model in ('IGCN', 'AttIGCN', 'IMF')
     tr = T.get_trainer({'name': 'IGCNTrainer' if igcn else 'BPRTrainer', 'optimizer': 'Adam', 'lr': 1e-3,
                         'l2_reg': args.l2_reg, 'aux_reg': 0.01, 'device': dev, 'n_epochs': 1, 'batch_size': args.batch,
                         'test_batch_size': 512, 'topks': [20]}, ds, m)

@@ -10,9 +10,13 @@ Steps chain like get_rep's layers (the input of step s+1 is the output of
 step s), so a step's item all-reduce is waited for by the next step's
 user-side SpMM.  Inputs are resident in HBM before the timed region.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 via
-torch.distributed.run (one process per GPU, RCCL over xGMI).  Rank 0 prints
-ONE JSON line.  The CPU baseline (rank 0, N = 1 only) times two CPU
+Launch: python bench.py [--gpus N --steps K --warmup W].  For N > 1 the ranks
+are one process per GPU (RCCL over xGMI): either a launcher starts them
+(python -m torch.distributed.run ... bench.py --gpus N: RANK / WORLD_SIZE
+are then set), or bench.py, invoked as a single process, starts them itself
+as children before it touches a GPU (igr.launch) and exits with their code.
+Rank 0 prints ONE JSON line.  Set-up is rank-local: every rank draws the
+same pair stream, counts one slice of it, and builds only its own shard.  The CPU baseline (rank 0, N = 1 only) times two CPU
 restatements of DGL's gspmm (torch.sparse.mm over CSR, and the oracle's C
 OpenMP SpMMSumCsr) for 3 passes each over the whole graph and reports the
 faster one.
@@ -145,6 +149,11 @@ def main():
                     help='map every rank to cuda:0 (multi-rank rehearsal on a one-GPU box, with --dist-backend gloo)')
     args = ap.parse_args()
 
+    from igr.launch import maybe_launch
+    rc = maybe_launch(__file__, sys.argv[1:], args.gpus, one_device=args.one_device)
+    if rc is not None:  # this process only started the ranks and waited for them
+        sys.exit(rc)
+
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local_rank = int(os.environ.get('LOCAL_RANK', 0))
@@ -167,14 +176,17 @@ def main():
     U, I, E, d = args.n_users, args.n_items, args.n_edges, args.d
     t0 = time.time()
     log(f'rank {rank}/{world}: drawing {E} interactions (U={U}, I={I}, {args.item_dist}, seed {args.seed})')
-    pairs = synthetic_pairs(U, I, E, args.seed, args.item_dist)
+    su, si = synthetic_pairs(U, I, E, args.seed, args.item_dist, stacked=False)
     side = sharded_side(U, I, args.replicate)
     SU, SI = (U, I) if side == 'users' else (I, U)  # the shard cuts its first side into ranges
     if side == 'items':
-        pairs = np.ascontiguousarray(pairs[:, ::-1])
+        su, si = si, su
+    setup = {'draw_s': time.time() - t0}
     log(f'building shard (C++ CSR build; {side} sharded) ... {time.time() - t0:.1f}s')
-    shard = BipartiteShard(pairs, SU, SI, rank, world, dev, d=d, item_tiles=args.item_tiles)
-    del pairs
+    shard = BipartiteShard.from_stream(su, si, SU, SI, rank, world, dev, timings=setup, d=d,
+                                       item_tiles=args.item_tiles)
+    del su, si
+    setup['total_s'] = time.time() - t0
     nu = shard.u1 - shard.u0
     log(f'shard users [{shard.u0}, {shard.u1}) local nnz {shard.local_nnz} '
         f'(user block {shard.user_block}, item block nnz {shard.item_nnz} in {len(shard.chunks)} row chunks) '
@@ -259,8 +271,18 @@ def main():
         ex = torch.tensor([exposed_ms, compute_ms], dtype=torch.float64, device=sdev)
         dist.all_reduce(ex, op=dist.ReduceOp.MAX)
         exposed_ms, compute_ms = float(ex[0]), float(ex[1])
+        keys = sorted(setup)
+        st = torch.zeros(world, len(keys), dtype=torch.float64, device=sdev)
+        st[rank] = torch.tensor([setup[k] for k in keys], dtype=torch.float64)
+        dist.all_reduce(st, op=dist.ReduceOp.SUM)
+        setup_ranks = [{k: round(float(st[r, j]), 3) for j, k in enumerate(keys)} for r in range(world)]
+        backend = dist.get_backend()
     else:
         total_nnz = shard.local_nnz
+        setup_ranks = [{k: round(float(v), 3) for k, v in sorted(setup.items())}]
+        backend = None
+    exchange = {'nccl': 'RCCL all-reduce', 'gloo': 'gloo all-reduce staged through host memory (rehearsal)',
+                None: 'no exchange (one rank)'}.get(backend, f'{backend} all-reduce')
     value = total_nnz * args.steps / elapsed
     avg_kernel_s = float(kern_ms.mean()) / 1e3
     avg_bytes = float(np.mean(launch_bytes))
@@ -300,7 +322,9 @@ def main():
                                    f'steps chained as propagation layers',
                        'n_users': U, 'n_items': I, 'n_draws': E, 'nnz': total_nnz, 'd': d,
                        'parallelism': (f'{side[:-1]}-range shards x{world}, '
-                                       f'{"item" if side == "users" else "user"} block replicated, RCCL all-reduce'),
+                                       f'{"item" if side == "users" else "user"} block replicated, {exchange}'),
+                       'dist_backend': backend, 'world_size': world,
+                       'devices': 'all ranks on cuda:0' if (args.one_device and world > 1) else 'one per rank',
                        'item_source_tiles': shard.item_tiles, 'launches_per_step': nl},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBPS, 'traffic': traffic,
@@ -319,7 +343,11 @@ def main():
                                           'algorithmic_GBps': launch_bytes[k] / float(kern_ms[:, k].mean()) / 1e6}
                                       for k, (n, _g, _s, r, z) in enumerate(launches)}},
             'cpu_baseline': cpu,
-            'per_rank': {'spmm_ms_per_step_max': compute_ms, 'exposed_exchange_ms_per_step_max': exposed_ms,
+            'per_rank': {'setup_s': setup_ranks,
+                         'setup_note': 'draw_s: the whole pair stream (every rank); count_s: degrees of one slice + '
+                                       'host all-reduce; select_s: own user range; build_s: CSR builds + copies of '
+                                       'the own shard',
+                         'spmm_ms_per_step_max': compute_ms, 'exposed_exchange_ms_per_step_max': exposed_ms,
                          'note': 'HIP events on the compute stream; steps chain as propagation layers and the '
                                  'exposed exchange is the compute stream\'s wait for the previous step\'s item '
                                  'all-reduces before its user-side SpMM, plus the final wait (0 at N = 1)'},

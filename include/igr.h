@@ -143,6 +143,22 @@ int igr_plan_fill(int64_t n_rows, const int64_t *row_ptr, int64_t split_threshol
                   int64_t chunk_edges, int64_t window, int32_t *order, int32_t *split_row,
                   int64_t *split_ptr, int32_t *chunk_row, int64_t *chunk_beg);
 
+/* Occurrences of each id: counts[b] = #{i : ids[i] == b}, b in [0, n_bins).
+ * The degree pass of utils.py:42-50 (a duplicate pair counts twice, as scipy's
+ * summed duplicates do in the row sum of model.py:90) over one slice of an
+ * interaction stream: the ranks of a sharded graph each count a slice and add
+ * the counts up.  An id outside [0, n_bins) is an error. */
+int igr_count_ids(int64_t n, const int64_t *ids, int64_t n_bins, int64_t *counts, int32_t n_threads);
+
+/* The pairs of an interaction stream whose key lies in [lo, hi), in stream
+ * order: out_key = key - lo, out_other = other.  *n_out receives the count;
+ * with out_key == out_other == NULL only the count is computed (call once to
+ * size the arrays, once to fill them).  This is how a rank of a sharded graph
+ * keeps its own user range of the training pairs (the reference holds the
+ * whole list in one process, dataset.py:94-114). */
+int igr_select_id_range(int64_t n, const int64_t *key, const int64_t *other, int64_t lo, int64_t hi,
+                        int64_t *out_key, int64_t *out_other, int64_t *n_out, int32_t n_threads);
+
 /* ------------------------------------------------------- device kernels */
 
 /* gspmm(g, 'mul', 'sum', lhs_data=x, rhs_data=rhs) - CSR SpMM, fp32.

@@ -46,6 +46,15 @@ static void parallel_for(int64_t n, int nt, F &&fn) {
     for (auto &t : ts) t.join();
 }
 
+// fn(t) for t in [0, nt), one thread each (the caller's thread takes t = 0).
+template <class F>
+static void per_thread(int nt, F &&fn) {
+    std::vector<std::thread> ts;
+    for (int t = 1; t < nt; ++t) ts.emplace_back([&fn, t]() { fn(t); });
+    fn(0);
+    for (auto &t : ts) t.join();
+}
+
 // Exclusive prefix sum of counts[0..n) into ptr[0..n].
 static void prefix(const int64_t *counts, int64_t n, int64_t *ptr) {
     ptr[0] = 0;
@@ -136,6 +145,61 @@ extern "C" int igr_csr_from_coo(int64_t n_rows, int64_t n_cols, int64_t nnz, con
             }
         });
         *nnz_out = row_ptr[n_rows];
+        return IGR_OK;
+    });
+}
+
+extern "C" int igr_count_ids(int64_t n, const int64_t *ids, int64_t n_bins, int64_t *counts,
+                             int32_t n_threads) {
+    return guarded("igr_count_ids", [&]() -> int {
+        const char *fn = "igr_count_ids";
+        if (n < 0 || n_bins < 0 || (n > 0 && !ids) || (n_bins > 0 && !counts)) return arg_error(fn, "bad args");
+        const int nt = resolve_threads(n_threads);
+        std::memset(counts, 0, sizeof(int64_t) * (size_t)n_bins);
+        std::atomic<int64_t> bad{-1};
+        parallel_for(n, nt, [&](int64_t b, int64_t e) {
+            for (int64_t i = b; i < e; ++i) {
+                const int64_t k = ids[i];
+                if (k < 0 || k >= n_bins) {
+                    bad.store(i);
+                    return;
+                }
+                __atomic_fetch_add(&counts[k], 1, __ATOMIC_RELAXED);
+            }
+        });
+        if (bad.load() >= 0) return arg_error(fn, "id out of range at position " + std::to_string(bad.load()));
+        return IGR_OK;
+    });
+}
+
+extern "C" int igr_select_id_range(int64_t n, const int64_t *key, const int64_t *other, int64_t lo, int64_t hi,
+                                   int64_t *out_key, int64_t *out_other, int64_t *n_out, int32_t n_threads) {
+    return guarded("igr_select_id_range", [&]() -> int {
+        const char *fn = "igr_select_id_range";
+        if (n < 0 || !n_out || (n > 0 && !key)) return arg_error(fn, "bad args");
+        if ((out_key == nullptr) != (out_other == nullptr) || (out_other && !other))
+            return arg_error(fn, "out_key / out_other (and other) go together");
+        // slices of the stream, one per thread: count, offsets, then an in-order copy
+        const int nt = std::max(1, resolve_threads(n_threads));
+        const int64_t step = (n + nt - 1) / nt;
+        std::vector<int64_t> cnt(nt + 1, 0);
+        per_thread(nt, [&](int t) {
+            int64_t c = 0;
+            for (int64_t i = t * step, e = std::min(n, (t + 1) * step); i < e; ++i) c += key[i] >= lo && key[i] < hi;
+            cnt[t + 1] = c;
+        });
+        for (int t = 0; t < nt; ++t) cnt[t + 1] += cnt[t];
+        *n_out = cnt[nt];
+        if (!out_key) return IGR_OK;
+        per_thread(nt, [&](int t) {
+            int64_t o = cnt[t];
+            for (int64_t i = t * step, e = std::min(n, (t + 1) * step); i < e; ++i)
+                if (key[i] >= lo && key[i] < hi) {
+                    out_key[o] = key[i] - lo;
+                    out_other[o] = other[i];
+                    ++o;
+                }
+        });
         return IGR_OK;
     });
 }

@@ -54,6 +54,8 @@ SIGNATURES = {
     'igr_device_info': (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_int), _P(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]),
     'igr_csr_from_coo': (ctypes.c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
                                         _P(c_i64), c_i32]),
+    'igr_count_ids': (ctypes.c_int, [c_i64, c_vp, c_i64, c_vp, c_i32]),
+    'igr_select_id_range': (ctypes.c_int, [c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, _P(c_i64), c_i32]),
     'igr_csr_transpose': (ctypes.c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32]),
     'igr_csr_row_sums': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp]),
     'igr_sym_norm_values': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -42,3 +42,17 @@ def all_gather_into(out, t, group=None):
         return out
     dist.all_gather_into_tensor(out, t.contiguous(), group=group)
     return out
+
+
+def all_reduce_sum_host(a, group=None, device=None):
+    """numpy int64 / float array -> its sum over ranks (set-up data that lives on the
+    host).  gloo reduces it where it is; RCCL reduces device tensors, so the array
+    makes a round trip through `device`."""
+    import numpy as np
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dist.get_backend(group) == 'gloo':
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        return t.numpy()
+    td = t.to(device)
+    dist.all_reduce(td, op=dist.ReduceOp.SUM, group=group)
+    return td.cpu().numpy()

@@ -352,8 +352,9 @@ class SyntheticDataset(BasicDataset):
         self._train_data = v
 
 
-def synthetic_pairs(n_users, n_items, n_edges, seed=0, item_dist='uniform', zipf_s=1.1):
-    """int64 [n_edges, 2] (user, item) draws with torch's CPU generator."""
+def synthetic_pairs(n_users, n_items, n_edges, seed=0, item_dist='uniform', zipf_s=1.1, stacked=True):
+    """int64 [n_edges, 2] (user, item) draws with torch's CPU generator; stacked=False
+    returns the two int64 arrays (users, items) of the same draws instead."""
     import torch
     g = torch.Generator().manual_seed(seed)
     u = torch.randint(0, n_users, (n_edges,), generator=g, dtype=torch.int64)
@@ -364,6 +365,8 @@ def synthetic_pairs(n_users, n_items, n_edges, seed=0, item_dist='uniform', zipf
         i = torch.multinomial(w / w.sum(), n_edges, replacement=True, generator=g)
     else:
         raise ValueError(item_dist)
+    if not stacked:
+        return u.numpy(), i.numpy()
     return torch.stack([u, i], 1).numpy()
 
 

@@ -27,7 +27,7 @@ import os
 import numpy as np
 import torch
 from . import comm, ops
-from .graph import Graph, TiledGraph, csr_from_coo, sym_norm_values
+from .graph import Graph, count_ids, csr_from_coo, csr_transpose, select_id_range, sym_norm_values
 
 MALL_BYTES = 256 << 20  # MI355X Infinity Cache
 
@@ -78,21 +78,26 @@ class BipartiteShard:
     """
 
     def __init__(self, pairs, n_users, n_items, rank, world, device, degree=None, d=64, item_tiles='auto',
-                 item_chunks='auto'):
+                 item_chunks='auto', local_pairs=None):
+        """pairs: int64 [n, 2] or a (users, items) tuple of int64 arrays.  local_pairs
+        (with `degree`): (users - u0, items) of this rank's own range only, already
+        selected - what from_stream hands over; `pairs` is then not read."""
         self.n_users, self.n_items = n_users, n_items
         self.rank, self.world = rank, world
-        u, i = pairs[:, 0], pairs[:, 1]
+        # the layer all-reduces its item partials; a test may switch it on at world 1 to run
+        # the exchange pattern through a one-rank process group
+        self.exchange = world > 1
+        if local_pairs is None:
+            u, i = (pairs[:, 0], pairs[:, 1]) if isinstance(pairs, np.ndarray) else pairs
         if degree is None:
             # duplicates count with multiplicity, as scipy sums them into the degree
-            degree = np.bincount(u, minlength=n_users).astype(np.float32)
-            degree = np.concatenate([degree, np.bincount(i, minlength=n_items).astype(np.float32)])
+            degree = np.concatenate([count_ids(u, n_users), count_ids(i, n_items)]).astype(np.float32)
         self.degree = degree
         self.dinv = np.power(np.maximum(np.float32(1.), degree), np.float32(-0.5)).astype(np.float32)
         self.ranges = balanced_ranges(degree[:n_users], world)
         u0, u1 = self.ranges[rank]
         self.u0, self.u1 = u0, u1
-        mine = (u >= u0) & (u < u1)
-        lu, li = u[mine] - u0, i[mine]
+        lu, li = select_id_range(u, i, u0, u1) if local_pairs is None else local_pairs
         nu = u1 - u0
         # user block: rows = local users, cols = items
         rp, ci, v, _ = csr_from_coo(lu, li, nu, n_items, None, dedup=True, want_eid=False)
@@ -100,12 +105,8 @@ class BipartiteShard:
         vals = sym_norm_values(rp, ci, v, dinv_u, dinv_i)
         self.user_block = Graph(rp, ci, nu, n_items, device=device)
         self.user_vals = torch.from_numpy(vals).to(device)
-        # item block: rows = items, cols = local users
-        rp2, ci2, v2, _ = csr_from_coo(li, lu, n_items, nu, None, dedup=True, want_eid=False)
-        vals2 = sym_norm_values(rp2, ci2, v2, dinv_i, dinv_u)
-        self.item_host = dict(row_ptr=rp2, col_idx=ci2, vals=vals2)
-        self.item_nnz = int(rp2[-1])
-        self.local_nnz = self.user_block.nnz + self.item_nnz
+        self._user_counts, self._dinv_u, self._dinv_i = v, dinv_u, dinv_i
+        self._item_host = None
         # source tiles: ~640 MB slices when the user table dwarfs the item output and the
         # Infinity Cache (measured on MI355X at 10M x 1M, d = 64: 8.2 -> 7.7 ms at T = 4)
         T = item_tiles
@@ -121,19 +122,69 @@ class BipartiteShard:
         # all-reduces the same row ranges
         cuts = _align32(balanced_ranges(degree[n_users:], self.item_chunks), n_items)
         col_bounds = [min(nu, 32 * int(round(k * nu / self.item_tiles / 32))) for k in range(self.item_tiles)] + [nu]
+        # item block: rows = items, cols = local users.  Each source tile is the transpose
+        # of a range of user rows (the user block is sorted, so the transposed rows come
+        # out sorted by user); a row chunk is a row range of every tile.
+        tile_csr = []
+        for t in range(self.item_tiles):
+            b0, b1 = col_bounds[t], col_bounds[t + 1]
+            tile_csr.append(self._transpose_users(b0, b1))
+        self.item_nnz = sum(int(t_rp[-1]) for t_rp, _, _ in tile_csr)
+        if self.item_tiles == 1:
+            self._item_host = dict(zip(('row_ptr', 'col_idx', 'vals'), tile_csr[0]))
+        self.local_nnz = self.user_block.nnz + self.item_nnz
         self.chunks = []  # (r0, r1, [(graph, vals, c0, c1), ...])
         for r0, r1 in cuts:
-            e0, e1 = int(rp2[r0]), int(rp2[r1])
-            crp = (rp2[r0:r1 + 1] - e0).astype(np.int64)
-            cci = ci2[e0:e1]
-            cv = torch.from_numpy(vals2[e0:e1]).to(device)
-            if self.item_tiles == 1:
-                tiles = [(Graph(crp, cci, r1 - r0, nu, device=device), cv, 0, nu)]
-            else:
-                tg = TiledGraph(dict(row_ptr=crp, col_idx=cci), r1 - r0, nu, col_bounds, device)
-                tiles = [(g, v, col_bounds[t], col_bounds[t + 1]) for t, (g, v) in
-                         enumerate(zip(tg.tiles, tg.tile_values(cv)))]
+            tiles = []
+            for t, (t_rp, t_ci, t_v) in enumerate(tile_csr):
+                e0, e1 = int(t_rp[r0]), int(t_rp[r1])
+                g = Graph(t_rp[r0:r1 + 1] - e0, t_ci[e0:e1], r1 - r0, col_bounds[t + 1] - col_bounds[t], device=device)
+                tiles.append((g, torch.from_numpy(t_v[e0:e1]).to(device), col_bounds[t], col_bounds[t + 1]))
             self.chunks.append((r0, r1, tiles))
+
+    def _transpose_users(self, b0, b1):
+        """(row_ptr, col_idx, vals) of A[I, b0:b1): the item rows over the local users
+        [b0, b1), columns relative to b0, values (dinv_i * a) * dinv_u (model.py:91-96)."""
+        h = self.user_block.host()
+        rp, ci = h['row_ptr'], h['col_idx']
+        e0, e1 = int(rp[b0]), int(rp[b1])
+        t_rp, t_ci, t_pos = csr_transpose(rp[b0:b1 + 1] - e0, ci[e0:e1], b1 - b0, self.n_items)
+        # multi-threaded gather of the duplicate counts into transposed order
+        a = torch.from_numpy(self._user_counts[e0:e1]).index_select(0, torch.from_numpy(t_pos)).numpy()
+        return t_rp, t_ci, sym_norm_values(t_rp, t_ci, a, self._dinv_i, self._dinv_u[b0:b1])
+
+    @property
+    def item_host(self):
+        """The whole item block as one host CSR: dict(row_ptr, col_idx, vals)."""
+        if self._item_host is None:
+            self._item_host = dict(zip(('row_ptr', 'col_idx', 'vals'), self._transpose_users(0, self.u1 - self.u0)))
+        return self._item_host
+
+    @classmethod
+    def from_stream(cls, users, items, n_users, n_items, rank, world, device, group=None, timings=None, **kw):
+        """A shard built from an interaction stream every rank holds (drawn from one
+        seed, or read from one file) with the counting and the CSR builds divided
+        among the ranks: rank k counts the degrees of the k-th slice of the stream,
+        the counts are added up across the ranks (one host all-reduce of
+        n_users + n_items integers), and each rank then selects and sorts only the
+        interactions of its own user range.  Needs an initialised process group
+        when world > 1.  timings: dict that receives the seconds of each stage."""
+        import time
+        t0 = time.perf_counter()
+        E = len(users)
+        e0, e1 = E * rank // world, E * (rank + 1) // world
+        counts = np.concatenate([count_ids(users[e0:e1], n_users), count_ids(items[e0:e1], n_items)])
+        if world > 1:
+            counts = comm.all_reduce_sum_host(counts, group, device)
+        degree = counts.astype(np.float32)
+        t1 = time.perf_counter()
+        u0, u1 = balanced_ranges(degree[:n_users], world)[rank]
+        local = select_id_range(users, items, u0, u1)
+        t2 = time.perf_counter()
+        sh = cls(None, n_users, n_items, rank, world, device, degree=degree, local_pairs=local, **kw)
+        if timings is not None:
+            timings.update(count_s=t1 - t0, select_s=t2 - t1, build_s=time.perf_counter() - t2)
+        return sh
 
     @property
     def item_block(self):
@@ -213,7 +264,7 @@ class BipartiteShard:
                         spmm(g, x_users[c0:c1, sl], v, yk[:, sl], t > 0, **kw)
                 hook(i, 'end')
                 i += 1
-            if self.world > 1:
+            if self.exchange:
                 works.append(comm.all_reduce_sum(yk, group, async_op=True))
         if y_users is None:
             y_users = torch.empty(self.u1 - self.u0, x_items.shape[1], dtype=torch.float32, device=x_items.device)

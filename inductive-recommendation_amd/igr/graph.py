@@ -57,6 +57,27 @@ def csr_from_coo(row, col, n_rows, n_cols, val=None, dedup=True, n_threads=0, wa
     return row_ptr, col_idx[:k].copy(), val_out[:k].copy(), None if eid is None else eid[:k].copy()
 
 
+def count_ids(ids, n_bins, n_threads=0):
+    """int64[n_bins]: occurrences of each id (np.bincount, multi-threaded)."""
+    ids = _np(ids, np.int64)
+    out = np.empty(n_bins, np.int64)
+    L.call('igr_count_ids', len(ids), _ptr(ids), n_bins, _ptr(out), n_threads)
+    return out
+
+
+def select_id_range(key, other, lo, hi, n_threads=0):
+    """(key - lo, other) for the pairs with lo <= key < hi, in input order."""
+    key, other = _np(key, np.int64), _np(other, np.int64)
+    assert len(key) == len(other)
+    n = ctypes.c_int64(0)
+    L.call('igr_select_id_range', len(key), _ptr(key), _ptr(other), lo, hi, None, None, ctypes.byref(n), n_threads)
+    ok, oo = np.empty(n.value, np.int64), np.empty(n.value, np.int64)
+    if n.value:
+        L.call('igr_select_id_range', len(key), _ptr(key), _ptr(other), lo, hi, _ptr(ok), _ptr(oo), ctypes.byref(n),
+               n_threads)
+    return ok, oo
+
+
 def csr_transpose(row_ptr, col_idx, n_rows, n_cols, n_threads=0):
     """Reverse graph: (t_row_ptr, t_col_idx, t_pos) with t_pos = forward CSR position."""
     row_ptr, col_idx = _np(row_ptr, np.int64), _np(col_idx, np.int32)

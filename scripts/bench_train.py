@@ -38,19 +38,27 @@ def main():
     ap.add_argument('--one-device', action='store_true',
                     help='every rank on cuda:0 (multi-rank rehearsal on a one-GPU box, with --dist-backend gloo)')
     ap.add_argument('--sharded', action='store_true',
-                    help='igr.dist_train.ShardedIGCN (one rank per GPU under torch.distributed.run; '
-                         'per-rank batch --batch)')
+                    help='igr.dist_train.ShardedIGCN, one rank per GPU (per-rank batch --batch): under '
+                         'torch.distributed.run, or with --gpus N this script starts the N ranks itself')
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='ranks of the --sharded run (default: WORLD_SIZE when launched, else 1)')
     ap.add_argument('--item-dist', default='uniform', choices=['uniform', 'zipf'],
                     help='item popularity of the synthetic draws (zipf: exponent 1.1)')
     ap.add_argument('--skewed', default=None, metavar='SHAPE',
                     help="MovieLens-like item popularity: the training pairs of tests/golden/ml_like.py's SHAPE "
                          "('ml100k', 'ml1m', 'ml1m_l3', 'gowalla') instead of uniform draws (sets users / items / d / layers)")
     args = ap.parse_args()
+    if args.sharded and args.gpus:
+        from igr.launch import maybe_launch
+        rc = maybe_launch(__file__, sys.argv[1:], args.gpus, one_device=args.one_device)
+        if rc is not None:  # this process only started the ranks and waited for them
+            sys.exit(rc)
     from igr import model as M
     from igr import trainer as T
     from igr.dataset import synthetic_pairs
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
+    assert not (args.sharded and args.gpus) or world == args.gpus, f'--gpus {args.gpus} but WORLD_SIZE={world}'
     if args.sharded and world > 1:
         import torch.distributed as dist
         local = 0 if args.one_device else int(os.environ.get('LOCAL_RANK', '0'))

@@ -346,3 +346,85 @@ def test_swapped_sides_layer_matches_oracle():
     ref = O.spmm(A, x.numpy())
     np.testing.assert_allclose(y_users.numpy(), ref[:U], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(y_items.numpy(), ref[U:], rtol=1e-5, atol=1e-6)
+
+
+# ------------------------------------------------------------------ rank-local set-up (BipartiteShard.from_stream)
+
+def _stream_worker(rank, world, port, pairs, U, I, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        tm = {}
+        a = BipartiteShard.from_stream(pairs[:, 0].copy(), pairs[:, 1].copy(), U, I, rank, world, 'cpu',
+                                       timings=tm, item_tiles=2, item_chunks=2)
+        b = BipartiteShard(pairs, U, I, rank, world, 'cpu', item_tiles=2, item_chunks=2)  # every rank counts everything
+        same = (a.u0, a.u1) == (b.u0, b.u1) and np.array_equal(a.degree, b.degree) and a.local_nnz == b.local_nnz
+        same = same and torch.equal(a.user_vals, b.user_vals)
+        for k in ('row_ptr', 'col_idx'):
+            same = same and np.array_equal(a.user_block.host()[k], b.user_block.host()[k])
+        for k in ('row_ptr', 'col_idx', 'vals'):
+            same = same and np.array_equal(a.item_host[k], b.item_host[k])
+        for (r0, r1, ta), (s0, s1, tb) in zip(a.chunks, b.chunks):
+            same = same and (r0, r1) == (s0, s1)
+            for (ga, va, c0, c1), (gb, vb, e0, e1) in zip(ta, tb):
+                same = same and (c0, c1) == (e0, e1) and torch.equal(va, vb)
+                same = same and np.array_equal(ga.host()['col_idx'], gb.host()['col_idx'])
+        q.put((rank, bool(same), sorted(tm), a.u0, a.u1, a.local_nnz))
+    except Exception:
+        import traceback
+        q.put((rank, 'error', traceback.format_exc()))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_from_stream_builds_the_same_shards(world):
+    """Counting one slice of the stream per rank + a host all-reduce + a range select
+    gives every rank exactly the shard the whole-list constructor builds."""
+    U, I, E = 900, 200, 20000
+    rng = np.random.default_rng(11)
+    pairs = np.stack([rng.integers(0, U, E), rng.integers(0, I, E)], 1)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stream_worker, args=(r, world, port, pairs, U, I, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    errs = [r[2] for r in res if r[1] == 'error']
+    assert not errs, errs[0]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res = sorted(res)
+    assert all(r[1] is True for r in res)
+    assert res[0][2] == ['build_s', 'count_s', 'select_s']
+    assert res[0][3] == 0 and res[-1][4] == U and all(a[4] == b[3] for a, b in zip(res, res[1:]))
+    assert sum(r[5] for r in res) == O.norm_adj(U, I, pairs).nnz
+
+
+def test_item_block_is_the_transposed_user_block():
+    """Each source tile of the item block is built by transposing a range of user rows:
+    together the tiles hold exactly the item rows of D^-1/2 A D^-1/2 (duplicate pairs summed)."""
+    U, I, E = 500, 90, 6000
+    rng = np.random.default_rng(3)
+    pairs = np.stack([rng.integers(0, U, E), rng.integers(0, I, E)], 1)  # E >> U*I/8: many duplicate pairs
+    A = O.norm_adj(U, I, pairs)
+    dense = np.zeros((U + I, U + I), np.float32)
+    rows = np.repeat(np.arange(U + I), np.diff(A.row_ptr))
+    dense[rows, A.col] = A.val
+    sh = BipartiteShard(pairs, U, I, 0, 1, 'cpu', item_tiles=3, item_chunks=2)
+    got = np.zeros((I, U), np.float32)
+    for r0, r1, tiles in sh.chunks:
+        for g, v, c0, c1 in tiles:
+            h = g.host()
+            rr = np.repeat(np.arange(r0, r1), np.diff(h['row_ptr']))
+            assert np.all(np.diff(h['row_ptr']) >= 0) and h['col_idx'].max(initial=0) < c1 - c0
+            got[rr, h['col_idx'] + c0] = v.numpy()
+    np.testing.assert_array_equal(got, dense[U:, :U])
+    ih = sh.item_host
+    full = np.zeros((I, U), np.float32)
+    full[np.repeat(np.arange(I), np.diff(ih['row_ptr'])), ih['col_idx']] = ih['vals']
+    np.testing.assert_array_equal(full, dense[U:, :U])

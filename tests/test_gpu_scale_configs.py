@@ -4,8 +4,11 @@
     Gowalla shape (29,858 x 40,981, ~1.04 M), d = 128, L = 3  IGCN     model.py:4188-4200, config.py:12-23
     synthetic scale, d = 256, the sharded layer with 128-column passes
     the bench workload itself (10 M x 1 M, 200 M draws, d = 64) through size-independent properties
+    the same graph at d = 256 (BASELINE's 8-GPU configuration's layer, here on one GPU), likewise
     the attention edge kernels on that graph's feature graph (nnz 411 M, 4 heads of d = 64), likewise
-    items outnumbering users (Amazon-Books-shaped), items sharded at world 2 on one GPU
+    items outnumbering users (Amazon-Books-shaped: 2.9 M items x 600 K users, d = 128), items cut
+    into ranges: at world 1 through the properties, at world 2 on one GPU against world 1; and a
+    tenth of that shape at world 2 against the float64 oracle
 
 The first two compare against fixtures written by tests/golden/make_scale_golden.py,
 which RAN the reference on the same inputs (data from tests/golden/ml_like.py,
@@ -199,68 +202,128 @@ def test_sharded_layer_d256_column_passes_at_scale():
     assert torch.equal(vu, yu) and torch.equal(vi, yi)
 
 
-def test_bench_workload_full_size_properties():
-    """The bench workload itself (10 M users x 1 M items, 200 M draws, d = 64: the graph, the
-    values and the launches bench.py times), checked through properties that need no
-    second full-size implementation:
+def _layer_properties(sh, d, seed=2, n_sample=200, single_pass_equal=False):
+    """One propagation layer of a world-1 shard, checked through properties that need no second
+    full-size implementation.  `cut` is the side the shard cuts into ranges (rows of
+    user_block), `rep` the replicated side:
       * a known answer: sqrt(degree) is an eigenvector of D^-1/2 A D^-1/2 with eigenvalue 1
         (utils.py:42-50), so layer(sqrt(deg)) = sqrt(deg) on every node with an interaction;
       * float64 on sampled rows of both sides, from the host CSR;
-      * the adjoint identity <x_u, A_ui x_i> = <A_iu x_u, x_i> ties the two blocks together;
+      * the adjoint identity <x_c, A_cr x_r> = <A_rc x_c, x_r> ties the two blocks together;
       * column checksums: 1^T (A x) = (A^T 1)^T x with the column sums of A taken on the host;
-      * linearity, and the same bits on a second run."""
+      * linearity, and the same bits on a second run;
+      * single_pass_equal: the 128-column passes of a wide layer change no bit."""
     from igr import dist
-    from igr.dataset import synthetic_pairs
-    U, I, E, d = 10_000_000, 1_000_000, 200_000_000, 64
-    pairs = synthetic_pairs(U, I, E, 0, 'uniform')
-    sh = dist.BipartiteShard(pairs, U, I, 0, 1, DEV, d=d)
-    del pairs
-    assert sh.local_nnz == 399_995_952 and sh.item_tiles == 4  # the graph and the tiling of the bench line
+    C, R = sh.u1 - sh.u0, sh.n_items
     deg = torch.from_numpy(sh.degree).to(DEV)
     # known answer (fp32 values: three roundings per edge, ~20 to ~200 terms per row)
-    su, si = deg[:U].sqrt()[:, None].repeat(1, d).contiguous(), deg[U:].sqrt()[:, None].repeat(1, d).contiguous()
-    eu, ei = sh.layer(su, si)
-    for got, ref in [(eu, su), (ei, si)]:
+    sc, sr = deg[:C].sqrt()[:, None].repeat(1, d).contiguous(), deg[C:].sqrt()[:, None].repeat(1, d).contiguous()
+    ec, er = sh.layer(sc, sr)
+    for got, ref in [(ec, sc), (er, sr)]:
         assert float(((got - ref).abs() / ref.clamp_min(1.0)).max()) <= 1e-5
-    del su, si, eu, ei
-    g = torch.Generator(device=DEV).manual_seed(2)
-    xu, xi = torch.randn(U, d, generator=g, device=DEV) * 0.1, torch.randn(I, d, generator=g, device=DEV) * 0.1
-    yu, yi = sh.layer(xu, xi)
+    del sc, sr, ec, er
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    xc, xr = torch.randn(C, d, generator=g, device=DEV) * 0.1, torch.randn(R, d, generator=g, device=DEV) * 0.1
+    yc, yr = sh.layer(xc, xr)
     # sampled rows in float64
     rng = np.random.default_rng(0)
     ub, ih = sh.user_block.host(), sh.item_host
     uv, iv = sh.user_vals.cpu().numpy(), ih['vals']
-    for r in rng.integers(0, U, 200):
+    for r in rng.integers(0, C, n_sample):
         b, e = int(ub['row_ptr'][r]), int(ub['row_ptr'][r + 1])
-        src = xi[torch.from_numpy(ub['col_idx'][b:e].astype(np.int64)).to(DEV)].cpu().numpy().astype(np.float64)
-        close(yu[r].cpu().numpy()[None], (uv[b:e, None].astype(np.float64) * src).sum(0)[None])
-    for r in rng.integers(0, I, 200):
+        src = xr[torch.from_numpy(ub['col_idx'][b:e].astype(np.int64)).to(DEV)].cpu().numpy().astype(np.float64)
+        close(yc[r].cpu().numpy()[None], (uv[b:e, None].astype(np.float64) * src).sum(0)[None], atol_row=2e-6)
+    heavy = np.argsort(np.diff(ih['row_ptr']))[-8:]  # the longest rows of the replicated side (split-row path)
+    for r in np.concatenate([rng.integers(0, R, n_sample), heavy]):
         b, e = int(ih['row_ptr'][r]), int(ih['row_ptr'][r + 1])
-        src = xu[torch.from_numpy(ih['col_idx'][b:e].astype(np.int64)).to(DEV)].cpu().numpy().astype(np.float64)
-        close(yi[r].cpu().numpy()[None], (iv[b:e, None].astype(np.float64) * src).sum(0)[None], atol_row=2e-6)
-    # adjoint identity between the user block and the item block (A symmetric)
-    lhs = float((xu.double() * yu.double()).sum())   # <x_u, A_ui x_i>
-    rhs = float((yi.double() * xi.double()).sum())   # <A_iu x_u, x_i>
-    scale = float((xu.double().abs() * yu.double().abs()).sum())
+        src = xc[torch.from_numpy(ih['col_idx'][b:e].astype(np.int64)).to(DEV)].cpu().numpy().astype(np.float64)
+        close(yr[r].cpu().numpy()[None], (iv[b:e, None].astype(np.float64) * src).sum(0)[None], atol_row=2e-6)
+    # adjoint identity between the two blocks (A symmetric)
+    lhs = float((xc.double() * yc.double()).sum())   # <x_c, A_cr x_r>
+    rhs = float((yr.double() * xr.double()).sum())   # <A_rc x_c, x_r>
+    scale = float((xc.double().abs() * yc.double().abs()).sum())
     assert abs(lhs - rhs) <= 1e-6 * scale
     # column checksums against host column sums of the values (float64)
-    cs_items = np.bincount(ub['col_idx'], weights=uv.astype(np.float64), minlength=I)   # A_ui^T 1
-    cs_users = np.bincount(ih['col_idx'], weights=iv.astype(np.float64), minlength=U)   # A_iu^T 1
-    for y, cs, x in [(yu, cs_items, xi), (yi, cs_users, xu)]:
+    cs_rep = np.bincount(ub['col_idx'], weights=uv.astype(np.float64), minlength=R)   # A_cr^T 1
+    cs_cut = np.bincount(ih['col_idx'], weights=iv.astype(np.float64), minlength=C)   # A_rc^T 1
+    for y, cs, x in [(yc, cs_rep, xr), (yr, cs_cut, xc)]:
         got = y.double().sum(0).cpu().numpy()
         w = torch.from_numpy(cs).to(DEV)
         ref = (w[:, None] * x.double()).sum(0).cpu().numpy()
         mag = float((w[:, None] * x.double().abs()).sum(0).max())
         assert np.abs(got - ref).max() <= 1e-6 * mag
+    del cs_rep, cs_cut
     # linearity and repeatability
-    zu, zi = torch.randn(U, d, generator=g, device=DEV) * 0.1, torch.randn(I, d, generator=g, device=DEV) * 0.1
-    wu, wi = sh.layer(zu, zi)
-    cu, ci = sh.layer(0.5 * xu - 2.0 * zu, 0.5 * xi - 2.0 * zi)
-    for got, a, b in [(cu, yu, wu), (ci, yi, wi)]:
+    zc, zr = torch.randn(C, d, generator=g, device=DEV) * 0.1, torch.randn(R, d, generator=g, device=DEV) * 0.1
+    wc, wr = sh.layer(zc, zr)
+    cc, cr = sh.layer(0.5 * xc - 2.0 * zc, 0.5 * xr - 2.0 * zr)
+    for got, a, b in [(cc, yc, wc), (cr, yr, wr)]:
         ref = 0.5 * a.double() - 2.0 * b.double()
         assert float((got.double() - ref).abs().max()) <= 2e-6 * float(ref.abs().max())
-    vu, vi = sh.layer(xu, xi)
-    assert torch.equal(vu, yu) and torch.equal(vi, yi)
+        del ref
+    del zc, zr, wc, wr, cc, cr
+    vc, vr = sh.layer(xc, xr)
+    assert torch.equal(vc, yc) and torch.equal(vr, yr)
+    if single_pass_equal:
+        one = dist._col_width
+        try:
+            dist._col_width = lambda d_, table_bytes: d_
+            vc, vr = sh.layer(xc, xr)
+        finally:
+            dist._col_width = one
+        assert torch.equal(vc, yc) and torch.equal(vr, yr)
+    return xc, xr, yc, yr
+
+
+_STREAM = {}
+
+
+def _bench_stream():
+    """The bench workload's pair stream (10 M users x 1 M items, 200 M draws, seed 0), drawn once."""
+    from igr.dataset import synthetic_pairs
+    if 'ui' not in _STREAM:
+        _STREAM['ui'] = synthetic_pairs(10_000_000, 1_000_000, 200_000_000, 0, 'uniform', stacked=False)
+    return _STREAM['ui']
+
+
+def test_bench_workload_full_size_properties():
+    """The bench workload itself (10 M users x 1 M items, 200 M draws, d = 64: the graph, the
+    values and the launches bench.py times; one layer is model.py:4193-4197) - see
+    _layer_properties."""
+    from igr import dist
+    U, I, d = 10_000_000, 1_000_000, 64
+    u, i = _bench_stream()
+    sh = dist.BipartiteShard.from_stream(u, i, U, I, 0, 1, DEV, d=d)
+    assert sh.local_nnz == 399_995_952 and sh.item_tiles == 4  # the graph and the tiling of the bench line
+    _layer_properties(sh, d)
+
+
+def test_synthetic_d256_full_size_properties():
+    """BASELINE configuration 5's layer at its full size: the same 10 M x 1 M x 200 M-draw graph
+    at d = 256 (one layer of model.py:4193-4197), which runs as two 128-column passes over
+    8 source tiles on the item side and over the 1 GB item table on the user side.  The
+    property set of _layer_properties, plus: the column passes change no bit against the
+    single-pass path, over the whole output."""
+    from igr import dist
+    U, I, d = 10_000_000, 1_000_000, 256
+    u, i = _bench_stream()
+    sh = dist.BipartiteShard.from_stream(u, i, U, I, 0, 1, DEV, d=d)
+    assert sh.local_nnz == 399_995_952 and sh.item_tiles == 8
+    assert dist._col_width(d, I * d * 4) == 128
+    _layer_properties(sh, d, seed=4, n_sample=100, single_pass_equal=True)
+    _STREAM.clear()
+
+
+def test_amazon_books_shape_full_size_properties():
+    """BASELINE configuration 4's graph at its size on one GPU: items outnumber users
+    (2.9 M items x 600 K users, 30 M draws with Zipf item popularity, d = 128; the layout the
+    Amazon loader produces, dataset.py:229-255), so the ITEMS are the side cut into ranges
+    and the user block is the replicated, all-reduced one (sharded_side).  World 1 here; the
+    world-2 run of the same graph is test_items_sharded_world2_full_size."""
+    from igr import dist
+    sh = _amazon_shard(0, 1, DEV)
+    assert sh.n_items == AM_U and sh.u1 - sh.u0 == AM_I  # the shard's cut side is the items
+    _layer_properties(sh, AM_D, seed=6)
 
 
 def test_attention_kernels_full_size_properties():
@@ -376,12 +439,108 @@ def test_igcn_forward_backward_adjoint_at_training_scale(mode):
 
 # ---------------------------------------------------------------- items outnumber users, items sharded (world 2)
 
-AM_U, AM_I, AM_E, AM_D = 52_000, 290_000, 3_000_000, 128
+AM_U, AM_I, AM_E, AM_D = 600_000, 2_900_000, 30_000_000, 128
+
+
+def _amazon_shard(rank, world, dev, group=None):
+    """Shard `rank` of the Amazon-Books-shaped graph, items cut into ranges."""
+    from igr.dataset import synthetic_pairs
+    from igr.dist import BipartiteShard, sharded_side
+    assert sharded_side(AM_U, AM_I, 'auto') == 'items'
+    u, i = synthetic_pairs(AM_U, AM_I, AM_E, 9, 'zipf', stacked=False)
+    return BipartiteShard.from_stream(i, u, AM_I, AM_U, rank, world, dev, group=group, d=AM_D)
+
+
+def _am_inputs(dev):
+    g = torch.Generator(device=dev).manual_seed(12)
+    return (torch.randn(AM_I, AM_D, generator=g, device=dev) * 0.1,
+            torch.randn(AM_U, AM_D, generator=g, device=dev) * 0.1)
+
+
+def _am_step(n_rows):
+    """Row sampling stride: ~3000 rows of a rank's range (Zipf popularity gives the first
+    rank a few hundred very long rows, the last one millions of short ones)."""
+    return max(1, n_rows // 3000)
+
+
+def _am_full_rank(rank, world, port, q):
+    import torch.distributed as tdist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    tdist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        dev = torch.device('cuda')
+        sh = _amazon_shard(rank, world, dev)
+        x_items, x_users = _am_inputs(dev)
+        y_own, y_rep = sh.layer(x_items[sh.u0:sh.u1].contiguous(), x_users)
+        y2_own, y2_rep = sh.propagate(x_items[sh.u0:sh.u1].contiguous(), x_users, 2)
+        torch.cuda.synchronize()
+        # hand back samples and checksums, not 1.8 GB of rows
+        rows_own = torch.arange(0, sh.u1 - sh.u0, _am_step(sh.u1 - sh.u0), device=dev)
+        q.put((rank, sh.u0, sh.u1, sh.local_nnz, y_own[rows_own].cpu().numpy(), y_rep.cpu().numpy(),
+               y2_own[rows_own].cpu().numpy(), y2_rep.cpu().numpy(),
+               y_own.double().sum(0).cpu().numpy(), y2_own.double().sum(0).cpu().numpy()))
+    except Exception:
+        import traceback
+        q.put((rank, 'error', traceback.format_exc()))
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_items_sharded_world2_full_size():
+    """BASELINE configuration 4 at its size as TWO ranks (both on the one GPU; gloo, staged
+    through host memory): rank-local set-up from the shared stream, one layer and two chained
+    layers with deferred reduces, against the world-1 shard of the same graph on this GPU:
+    the replicated user block must agree to fp32 reassociation of the two partial sums, the
+    unsplit item rows of each rank bit for bit (they are complete locally once x is the same)."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_am_full_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=120)
+    for r in res:
+        assert r[1] != 'error', r[2]
+    one = _amazon_shard(0, 1, DEV)
+    x_items, x_users = _am_inputs(DEV)
+    y_items, y_users = one.layer(x_items, x_users)
+    y2_items, y2_users = one.propagate(x_items, x_users, 2)
+    assert res[0][1] == 0 and res[-1][2] == AM_I and res[0][2] == res[1][1]
+    assert sum(r[3] for r in res) == one.local_nnz
+    tot1, tot2, n_short, n_split = np.zeros(AM_D), np.zeros(AM_D), 0, 0
+    deg_items = np.diff(one.user_block.host()['row_ptr'])
+    for rank, i0, i1, _nnz, y_own, y_rep, y2_own, y2_rep, s1, s2 in res:
+        rows = torch.arange(0, i1 - i0, _am_step(i1 - i0), device=DEV) + i0
+        # layer 1: an item row needs only x_users, so a rank's rows equal the world-1 rows bit
+        # for bit - except rows long enough to be split into chunks (> 512 edges), whose
+        # partial sums are added in a tree chosen from the shard's chunk statistics
+        want = y_items[rows].cpu().numpy()
+        short = deg_items[rows.cpu().numpy()] <= 512
+        n_short, n_split = n_short + int(short.sum()), n_split + int((~short).sum())
+        assert np.array_equal(y_own[short], want[short]), 'unsplit item rows differ between world 2 and world 1'
+        close(y_own, want, atol_row=2e-6)
+        close(y_rep, y_users.cpu().numpy(), atol_row=2e-6)
+        close(y2_own, y2_items[rows].cpu().numpy(), rtol=2e-5, atol_row=3e-6)
+        close(y2_rep, y2_users.cpu().numpy(), rtol=2e-5, atol_row=3e-6)
+        tot1 += s1
+        tot2 += s2
+    assert n_short > 1000 and n_split >= 1  # both kinds of row were compared
+    np.testing.assert_allclose(tot1, y_items.double().sum(0).cpu().numpy(), rtol=1e-6, atol=1e-5)  # split rows differ in the last bit
+    np.testing.assert_allclose(tot2, y2_items.double().sum(0).cpu().numpy(), rtol=1e-5, atol=1e-6)
+    # both ranks hold the same reduced user block, bit for bit
+    assert np.array_equal(res[0][5], res[1][5]) and np.array_equal(res[0][7], res[1][7])
+
+
+AMS_U, AMS_I, AMS_E = 52_000, 290_000, 3_000_000  # a tenth of the shape, against the float64 oracle
 
 
 def _amazon_pairs():
     from igr.dataset import synthetic_pairs
-    return synthetic_pairs(AM_U, AM_I, AM_E, 9, 'zipf')
+    return synthetic_pairs(AMS_U, AMS_I, AMS_E, 9, 'zipf')
 
 
 def _free_port():
@@ -401,13 +560,13 @@ def _am_rank(rank, world, port, q):
         from igr.dist import BipartiteShard, sharded_side
         dev = torch.device('cuda')
         pairs = _amazon_pairs()
-        side = sharded_side(AM_U, AM_I, 'auto')
+        side = sharded_side(AMS_U, AMS_I, 'auto')
         assert side == 'items'
         sw = np.ascontiguousarray(pairs[:, ::-1])  # the shard cuts its first side: items
-        sh = BipartiteShard(sw, AM_I, AM_U, rank, world, dev, d=AM_D)
+        sh = BipartiteShard(sw, AMS_I, AMS_U, rank, world, dev, d=AM_D)
         rng = np.random.default_rng(3)
-        x_items = (rng.standard_normal((AM_I, AM_D)) * 0.1).astype(np.float32)
-        x_users = (rng.standard_normal((AM_U, AM_D)) * 0.1).astype(np.float32)
+        x_items = (rng.standard_normal((AMS_I, AM_D)) * 0.1).astype(np.float32)
+        x_users = (rng.standard_normal((AMS_U, AM_D)) * 0.1).astype(np.float32)
         y_own, y_rep = sh.layer(torch.from_numpy(x_items[sh.u0:sh.u1]).to(dev), torch.from_numpy(x_users).to(dev))
         y1_own, y1_rep = sh.propagate(torch.from_numpy(x_items[sh.u0:sh.u1]).to(dev),
                                       torch.from_numpy(x_users).to(dev), 2)
@@ -439,18 +598,18 @@ def test_items_sharded_world2_one_gpu_matches_oracle():
     for r in res:
         assert r[1] != 'error', r[2]
     pairs = _amazon_pairs()
-    A = O.norm_adj(AM_U, AM_I, pairs)  # rows [users; items]
+    A = O.norm_adj(AMS_U, AMS_I, pairs)  # rows [users; items]
     rng = np.random.default_rng(3)
-    x_items = (rng.standard_normal((AM_I, AM_D)) * 0.1).astype(np.float32)
-    x_users = (rng.standard_normal((AM_U, AM_D)) * 0.1).astype(np.float32)
+    x_items = (rng.standard_normal((AMS_I, AM_D)) * 0.1).astype(np.float32)
+    x_users = (rng.standard_normal((AMS_U, AM_D)) * 0.1).astype(np.float32)
     x = np.concatenate([x_users, x_items])
     y = O.spmm64(A, x)
     y2 = _spmm64_f64(A, y)
-    assert res[0][1] == 0 and res[-1][2] == AM_I and res[0][2] == res[1][1]
+    assert res[0][1] == 0 and res[-1][2] == AMS_I and res[0][2] == res[1][1]
     for rank, i0, i1, y_own, y_rep, y2_own, y2_rep in res:
-        close(y_own, y[AM_U + i0:AM_U + i1], atol_row=2e-6)
-        close(y_rep, y[:AM_U], atol_row=2e-6)       # the replicated user block, all-reduced
-        close(y2_own, y2[AM_U + i0:AM_U + i1], rtol=2e-5, atol_row=3e-6)
-        close(y2_rep, y2[:AM_U], rtol=2e-5, atol_row=3e-6)
+        close(y_own, y[AMS_U + i0:AMS_U + i1], atol_row=2e-6)
+        close(y_rep, y[:AMS_U], atol_row=2e-6)       # the replicated user block, all-reduced
+        close(y2_own, y2[AMS_U + i0:AMS_U + i1], rtol=2e-5, atol_row=3e-6)
+        close(y2_rep, y2[:AMS_U], rtol=2e-5, atol_row=3e-6)
     # both ranks hold the same reduced user block, bit for bit
     assert np.array_equal(res[0][4], res[1][4]) and np.array_equal(res[0][6], res[1][6])

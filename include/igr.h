@@ -180,7 +180,9 @@ int igr_spmm_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx, const
  * igr_spmm_f32, bit for bit.  All calls on one GPU share that GPU's array:
  * calls that overlap on one GPU (two streams, two threads) race.  Nothing in
  * the array needs clearing between calls.  The first call on a device looks up
- * the array's address (make it outside a stream capture). */
+ * the array's address (make it outside a stream capture).  The device that owns
+ * the output must be the current one (hipSetDevice): the array is per device, and
+ * a call whose output lives on another GPU is rejected with IGR_ERR_ARG. */
 #define IGR_SPMM_NOALLOC_MAX_FLOATS (4 << 20)
 int igr_spmm_noalloc_f32(const igr_csr *g, int32_t d, const float *x, int64_t ldx, const float *rhs,
                          float *y, int64_t ldy, const igr_epilogue *epi, void *stream);

@@ -63,10 +63,15 @@ inline RowPlan row_plan_of(const igr_csr *g) {
 
 // A graph carries a usable schedule when its unsplit-row list and its chunk list are both
 // there (igr_plan_fill) and cover something.
+// It must also cover every row exactly once (unsplit rows + split rows = rows) and name
+// its split rows: a kernel that walks a partial plan would leave rows unwritten.
 inline bool has_row_plan(const igr_csr *g) {
     if (g->n_order + g->n_chunks <= 0) return false;
+    if (g->n_order + g->n_split != g->n_rows) return false;
     if (g->n_order > 0 && !g->order) return false;
     if (g->n_chunks > 0 && (!g->chunk_row || !g->chunk_beg || g->chunk_edges <= 0)) return false;
+    if ((g->n_split > 0) != (g->n_chunks > 0)) return false;
+    if (g->n_split > 0 && (!g->split_row || !g->split_ptr)) return false;
     return true;
 }
 

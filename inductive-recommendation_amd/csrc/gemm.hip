@@ -346,11 +346,7 @@ __global__ __launch_bounds__(256, IGR_GEMMP_OCC) void gemm_rows_persistent(int64
     auto store1 = [&](const f32x4 (&src)[NB][2], int64_t m0, int s, auto guard) __attribute__((always_inline)) {
         const int rb = s / NB, j = s % NB;
         const int64_t gm = m0 + 16 * rb + m16;
-#ifdef IGR_GEMMP_NOSTORE
-        if (gm < M && src[0][rb][0] == 12345.678f)
-#else
         if (!decltype(guard)::value || gm < M)
-#endif
             *reinterpret_cast<f32x4 *>(C + gm * ldc + n0 + 16 * j + 4 * g) = src[j][rb];
     };
     // MFMAs of rows [32 half, 32 half + 32) of the tile in As[buf] into dst; when STORE, the

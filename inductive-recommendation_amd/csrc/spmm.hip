@@ -671,7 +671,10 @@ constexpr int kMaxDevices = 64;
 static std::mutex g_scratch_mu;
 static float *g_scratch_ptr[kMaxDevices];  // per device, filled on first use
 
-static int scratch_for_current_device(const char *fn, float **out) {
+// The scratch array of the device that owns `owned` (a device pointer of the call: the
+// output).  hipGetSymbolAddress resolves the array for the CURRENT device, so that device
+// must be the pointer's: a launch on another GPU's stream with this GPU's array would fault.
+static int scratch_for_device_of(const char *fn, const void *owned, float **out) {
     int dev = -1;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) {
@@ -679,6 +682,18 @@ static int scratch_for_current_device(const char *fn, float **out) {
         return IGR_ERR_HIP;
     }
     if (dev < 0 || dev >= kMaxDevices) return arg_error(fn, "device index out of range");
+    hipPointerAttribute_t at{};
+    e = hipPointerGetAttributes(&at, owned);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // the failed query must not surface as a later launch error
+        return arg_error(fn, std::string("the output is not memory HIP knows (") + hipGetErrorString(e) + ")");
+    }
+    if (at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeManaged)
+        return arg_error(fn, "the output is not device memory");
+    if (at.device != dev)
+        return arg_error(fn, "the output lives on device " + std::to_string(at.device) + " but device " +
+                                 std::to_string(dev) + " is current: make the output's device current before the "
+                                 "call (each GPU has its own scratch array)");
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     if (!g_scratch_ptr[dev]) {
         void *p = nullptr;
@@ -711,7 +726,9 @@ extern "C" int igr_spmm_noalloc_f32(const igr_csr *g, int32_t d, const float *x,
         // every partial row the combine kernel reads is written by the main kernel
         // of the same call, so nothing in the array has to start at zero
         if (g->n_chunks > 0) {
-            const int rc = scratch_for_current_device(fn, &ws);
+            const void *owned = y ? (const void *)y : (epi ? (const void *)epi->acc : nullptr);
+            if (!owned) return arg_error(fn, "no output (y is NULL and the epilogue has no acc)");
+            const int rc = scratch_for_device_of(fn, owned, &ws);
             if (rc != IGR_OK) return rc;
         }
         if (!rhs) return run_spmm(fn, g, d, x, ldx, W_One{}, y, ldy, epi, ws, stream);

@@ -248,7 +248,6 @@ class Graph:
             v.edge_id = None
             v.csr = L.IgrCsr.from_buffer_copy(self.csr)
             v.csr.edge_id = None
-            v._reverse = None
             self._positional = v
         return v
 
@@ -256,6 +255,19 @@ class Graph:
         """Reverse graph for gspmm backward; its edge ids are this graph's edge ids."""
         base = getattr(self, '_base', None)
         if base is not None:
+            if self.edge_id is None and base.edge_id is not None:
+                # a positional view: its per-edge arrays are in this graph's CSR order, so the
+                # reverse must address them by forward CSR position (t_pos), not by the base
+                # graph's edge ids
+                rev = self.__dict__.get('_pos_reverse')
+                if rev is None:
+                    h = base._host
+                    t_rp, t_ci, t_pos = csr_transpose(h['row_ptr'], h['col_idx'], self.n_rows, self.n_cols)
+                    own = {} if base._auto_plan else dict(split_threshold=base.split_threshold,
+                                                          chunk_edges=base.chunk_edges)
+                    rev = Graph(t_rp, t_ci, self.n_cols, self.n_rows, device=self.device, edge_id=t_pos, **own)
+                    self._pos_reverse = rev
+                return rev
             return base.reverse()
         if self._reverse is None:
             h = self._host

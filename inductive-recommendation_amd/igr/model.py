@@ -123,6 +123,18 @@ class BasicModel(nn.Module):
         self.trainable = True
 
     @property
+    def graph_safe(self):
+        """May a training step of this model be captured in a hipGraph and replayed with the
+        same results as eager steps?  Yes when nothing in the step is drawn on the host or from
+        torch's generator: dropout masks from device counters (IGCN family, unless
+        dropout_rng = 'cpu'), or no dropout at all."""
+        if not torch.device(self.device).type == 'cuda':
+            return False
+        if isinstance(self, (IGCN, LightGCN)):
+            return self.config.get('dropout_rng', 'device') != 'cpu' or getattr(self, 'dropout', 0) == 0
+        return isinstance(self, (NGCF, IMCGAE)) and getattr(self, 'dropout', 0) == 0
+
+    @property
     def norm_vals(self):
         """The adjacency's edge values by edge id (the reference keeps them inside
         its sparse norm_adj; here they ride on the Graph generate_graph returns)."""
@@ -563,11 +575,26 @@ class IGCN(BasicModel):
             return None
         if getattr(self, '_aux_side', None) is None:
             self._aux_side = torch.cuda.Stream(device=self.embedding.weight.device)
-            # the table's gradient now arrives from two streams by design; autograd orders them
-            setter = getattr(torch.autograd.graph, 'set_warn_on_accumulate_grad_stream_mismatch', None)
-            if setter is not None:
-                setter(False)
         return self._aux_side
+
+    def backward_scope(self):
+        """Context for loss.backward() of a step whose aux term ran on the side stream: the
+        table's gradient then arrives from two streams by design (autograd orders them), and
+        autograd's warning about that is switched off for the backward only and switched back
+        on after it - not for the rest of the process."""
+        import contextlib
+        setter = getattr(torch.autograd.graph, 'set_warn_on_accumulate_grad_stream_mismatch', None)
+        if getattr(self, '_aux_side', None) is None or setter is None:
+            return contextlib.nullcontext()
+
+        @contextlib.contextmanager
+        def scope():
+            setter(False)
+            try:
+                yield
+            finally:
+                setter(True)  # torch's default
+        return scope()
 
     def aux_loss(self, users, pos_items, neg_items):
         """IGCNTrainer aux term (trainer.py:542-549) on the raw feature table with w."""

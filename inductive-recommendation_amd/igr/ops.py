@@ -29,6 +29,15 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def _written(out, fresh):
+    """A kernel wrote `out` through its raw pointer: tell autograd's version counter when the
+    buffer is the caller's (a value buffer reused across steps), so anything keyed on
+    tensor._version - the permuted-values cache of the gspmm backward - sees the write."""
+    if not fresh:
+        torch.autograd.graph.increment_version(out)
+    return out
+
+
 def _dev(*ts):
     for t in ts:
         if t is not None and not (isinstance(t, torch.Tensor) and t.is_cuda):
@@ -226,12 +235,13 @@ def dropout_uniforms(g: Graph, seed, offset, swap=False, offset_dev=None):
 
 def feat_row_values(row_sum, exponent, out=None):
     """Per-row row_sum ** exponent (IGCN.update_feat_mat's value, model.py:4127-4130)."""
+    fresh = out is None
     _dev(row_sum, out)
     out = torch.empty_like(row_sum) if out is None else out
     if out.numel() != row_sum.numel() or out.dtype != torch.float32 or not out.is_contiguous():
         raise IgrError(f'feat_row_values: out has {out.numel()} values for {row_sum.numel()} rows')
     L.call('igr_feat_values_f32', row_sum.numel(), None, _p(row_sum), float(exponent), _p(out), _stream())
-    return out
+    return _written(out, fresh)
 
 
 def _feat_spmm(feat, x, fw, out=None, epi=None, reverse=False):
@@ -394,6 +404,7 @@ def att_softmax_bwd(g: Graph, alpha, sqrt_d, rmax, rsum, dw, keep=None):
 def edge_dropout_counter(g: Graph, val, p, seed, offset, swap=False, offset_dev=None, out=None):
     """edge_dropout(val, dropout_uniforms(g, seed, offset, ...), p) in one pass, no rand array
     (igr_edge_dropout_counter_f32); val and out by edge id."""
+    fresh = out is None
     _dev(val, out, offset_dev)
     val = _f32(val).contiguous()
     if val.numel() != g.nnz:
@@ -402,20 +413,22 @@ def edge_dropout_counter(g: Graph, val, p, seed, offset, swap=False, offset_dev=
         out = torch.empty_like(val)
     L.call('igr_edge_dropout_counter_f32', ctypes.byref(g.csr), _p(val), float(p), ctypes.c_uint64(seed & (2 ** 64 - 1)),
            ctypes.c_uint64(offset & (2 ** 64 - 1)), _p(offset_dev), int(swap), _p(out), _stream())
-    return out
+    return _written(out, fresh)
 
 
 def edge_dropout(val, rand, p, out=None):
+    fresh = out is None
     _dev(val, rand, out)
     if rand.numel() != val.numel():
         raise IgrError('edge_dropout: rand and val sizes differ')
     if out is None:
         out = torch.empty_like(val)
     L.call('igr_edge_dropout_f32', val.numel(), _p(val), _p(rand), float(p), _p(out), _stream())
-    return out
+    return _written(out, fresh)
 
 
 def feat_values(g: Graph, row_sum, exponent, out=None):
+    fresh = out is None
     _dev(row_sum, out)
     if row_sum.numel() != g.n_rows:
         raise IgrError('feat_values: row_sum size differs from n_rows')
@@ -425,7 +438,7 @@ def feat_values(g: Graph, row_sum, exponent, out=None):
         raise IgrError(f'feat_values: out has {out.numel()} values, the graph has {g.nnz} edges '
                        f'(a buffer cached for another feature graph?)')
     L.call('igr_feat_values_f32', g.n_rows, _p(g.row_ptr), _p(row_sum), float(exponent), _p(out), _stream())
-    return out
+    return _written(out, fresh)
 
 
 def gather_rows(src, idx, offset=0):

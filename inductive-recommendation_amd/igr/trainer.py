@@ -12,9 +12,14 @@ eval mode both are the same function of the weights.
 
 Trainer config extensions (all optional): 'sampler': 'device' (default, HIP
 sampler, igr.sampler) or 'host' (vectorised numpy); 'fused' (default True);
-'seed'; 'graph' (default False): train_one_epoch replays one hipGraph-captured
-step (StepGraph) instead of issuing every launch from Python.  The epoch loss is accumulated on the device and read once per epoch
-(the reference syncs with loss.item() every step, trainer.py:556).
+'seed'; 'graph' (default 'auto'): train_one_epoch replays one hipGraph-captured
+step (StepGraph) instead of issuing every launch from Python.  'auto' takes the
+captured step where it is proven bitwise equal to eager steps (graph_mode_for:
+device sampler, fused losses, a model whose dropout masks come from device
+counters, an unsharded trainer on a ROCm device); True insists on it wherever the
+device sampler runs, False always steps eagerly.  The epoch loss is accumulated
+on the device and read once per epoch (the reference syncs with loss.item()
+every step, trainer.py:556).
 """
 import contextlib
 import ctypes
@@ -249,12 +254,19 @@ class BasicTrainer:
             self._step_graph = None
 
     def _graph_epoch(self):
-        """The epoch through a StepGraph when config['graph'] is set and the device
-        sampler is in use; None = run it eagerly (leaving graph mode first)."""
-        if self.config.get('graph', False) and isinstance(self.sampler, DeviceBPRSampler):
+        """The epoch through a StepGraph when graph_mode_for(self) says so; None = run it
+        eagerly (leaving graph mode first)."""
+        if graph_mode_for(self):
             return graph_epoch(self)
         self._close_step_graph()
         return None
+
+    def _eager_step_guard(self):
+        """A step() called from outside while a captured step is live (its counters are on
+        the device): hand the counters back to the host first, so eager and captured steps
+        can be mixed freely."""
+        if getattr(self, '_step_graph', None) is not None and not getattr(self, '_in_graph_body', False):
+            self._close_step_graph()
 
     def calculate_metrics(self, eval_data, rec_items):
         n_items = max(int(self.dataset.n_items), int(rec_items.max(initial=0)) + 1)
@@ -444,10 +456,14 @@ class StepGraph:
             u, p, ng = tr.sampler.sample(n, offset=self.s0, offset_dev=self.ctr)
             if self.aux is not None:
                 au, ap, an = self.aux.sample(n, offset=self.a0, offset_dev=self.ctr)
-        if self.aux is not None:
-            _summed_step(tr, self.loss_sum, n, u, p, ng, au, ap, an)
-        else:
-            _summed_step(tr, self.loss_sum, n, u, p, ng)
+        tr._in_graph_body = True
+        try:
+            if self.aux is not None:
+                _summed_step(tr, self.loss_sum, n, u, p, ng, au, ap, an)
+            else:
+                _summed_step(tr, self.loss_sum, n, u, p, ng)
+        finally:
+            tr._in_graph_body = False
         tr.model.__dict__.pop('_batch_stream', None)  # consumed by the model; never left behind
         L.call('igr_counter_add', ctypes.c_void_p(self.ctr.data_ptr()), 1, ops._stream())
         if count:
@@ -475,6 +491,23 @@ class StepGraph:
         tr.opt.advance_host_steps(self.n)
         model.device_step = None
         self.graph = self._keep = None
+
+
+def graph_mode_for(trainer):
+    """Does train_one_epoch replay a captured step?  config['graph']: True / False, or 'auto'
+    (the default): on exactly where the captured step has been shown bitwise equal to eager
+    steps - the device sampler draws the batches, the losses are the fused ones, the model's
+    dropout masks are counter-based (`graph_safe`: IGCN / IMF / AttIGCN / LightGCN unless
+    dropout_rng = 'cpu'; NGCF and IMCGAE only at dropout 0, their node dropout draws from
+    torch's generator), and the device is a GPU.  The sharded trainer (dist_train) has its own
+    loop and never comes here."""
+    want = trainer.config.get('graph', 'auto')
+    if not isinstance(trainer.sampler, DeviceBPRSampler):
+        return False  # host-drawn batches cannot be captured
+    if want != 'auto':
+        return bool(want)
+    return bool(getattr(trainer, 'fused', False)) and bool(getattr(trainer.model, 'graph_safe', False)) and \
+        hasattr(trainer.model, 'bpr_loss')
 
 
 def graph_epoch(trainer):
@@ -517,7 +550,9 @@ def fused_loss_step(trainer, bpr, l2, aux=None):
         terms.append(t)
         grads.append(cache[c])
     trainer.opt.zero_grad()
-    torch.autograd.backward(terms, grads)
+    scope = getattr(trainer.model, 'backward_scope', None)  # IGCN: the aux term's side stream
+    with (scope() if scope is not None else contextlib.nullcontext()):
+        torch.autograd.backward(terms, grads)
     trainer.opt.step()
     return loss
 
@@ -565,6 +600,7 @@ class BPRTrainer(BasicTrainer):
 
     def step(self, users, pos_items, neg_items):
         """One training step on a device batch; returns the loss tensor."""
+        self._eager_step_guard()
         if self.fused and hasattr(self.model, 'bpr_loss'):
             bpr_loss, l2 = self.model.bpr_loss(users, pos_items, neg_items, need_l2=self.l2_reg != 0)
             return fused_loss_step(self, bpr_loss, l2)
@@ -609,6 +645,7 @@ class IGCNTrainer(BasicTrainer):
         self.fused = trainer_config.get('fused', True)
 
     def step(self, users, pos_items, neg_items, a_users, a_pos, a_neg):
+        self._eager_step_guard()
         m = self.model
         if self.fused:
             bpr_loss, l2, aux_loss = m.bpr_aux_loss(users, pos_items, neg_items, a_users, a_pos, a_neg,

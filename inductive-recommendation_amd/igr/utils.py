@@ -1,8 +1,9 @@
 """igr.utils - the helpers of the reference's utils.py that its scripts and models
 call by name: run set-up (`set_seed`, `init_run`, utils.py:13-30) and graph
 construction (`generate_daj_mat`, `get_sparse_tensor`, `graph_rank_nodes`,
-utils.py:33-50, 186-215).  The epoch loss is accumulated on the device by the
-trainers, so no host-side meter is needed."""
+utils.py:33-50, 186-215), plus `AverageMeter` and `Unbuffered` (utils.py:280-305),
+which code written against the reference imports by name (the trainers here
+accumulate the epoch loss on the device and do not need a host-side meter)."""
 import os
 import random
 import sys
@@ -64,3 +65,40 @@ def graph_rank_nodes(dataset, ranking_metric):
     """utils.py:186-215 ('degree', 'sort' / 'greedy')."""
     from .model import graph_rank_nodes as rank
     return rank(dataset, ranking_metric)
+
+
+class AverageMeter:
+    """Running value / sum / count / average of a scalar (utils.py:280-295)."""
+
+    def __init__(self):
+        self.reset()
+
+    def reset(self):
+        self.val = self.avg = self.sum = self.count = 0
+
+    def update(self, val, n=1):
+        self.val = val
+        self.sum += val * n
+        self.count += n
+        self.avg = self.sum / self.count
+
+
+class Unbuffered:
+    """Wraps a text stream so that every write reaches the file at once (utils.py:291-305):
+    `sys.stdout = Unbuffered(sys.stdout)`.  Everything else is the wrapped stream's."""
+
+    def __init__(self, stream):
+        self.stream = stream
+
+    def _through(self, method, payload):
+        getattr(self.stream, method)(payload)
+        self.stream.flush()
+
+    def write(self, data):
+        self._through('write', data)
+
+    def writelines(self, datas):
+        self._through('writelines', datas)
+
+    def __getattr__(self, name):
+        return getattr(self.stream, name)

@@ -157,7 +157,20 @@ def test_reverse_graph_edge_ids():
     p = r.positional()
     assert p is r.positional() and p.edge_id is None and not p.csr.edge_id and r.csr.edge_id
     assert p.csr.row_ptr == r.csr.row_ptr and p.csr.col_idx == r.csr.col_idx and p.csr.n_chunks == r.csr.n_chunks
-    assert p._ws is r._ws and p.reverse() is r.reverse()
+    assert p._ws is r._ws
+    # the reverse of a positional view addresses per-edge data by the VIEW's order (CSR position
+    # of r), not by the input edge ids: with the values permuted once, it rebuilds the same matrix
+    pv = rng.standard_normal(400).astype(np.float32)          # values by input edge id
+    pos_vals = pv[rh['edge_id']]                              # ... permuted into r's CSR order
+    pr = p.reverse()
+    assert pr is p.reverse() and pr is not r.reverse()
+    prh = pr.host()
+    dense = np.zeros((pr.n_rows, pr.n_cols), np.float64)
+    np.add.at(dense, (np.repeat(np.arange(pr.n_rows), np.diff(prh['row_ptr'])), prh['col_idx']),
+              pos_vals[prh['edge_id']])
+    want = np.zeros_like(dense)
+    np.add.at(want, (dst, src), pv)                           # g: rows = dst, cols = src
+    np.testing.assert_allclose(dense, want, rtol=0, atol=1e-12)
     # values permuted once (vals[edge_id]) then read in order = values read through the edge ids
     vals = rng.standard_normal(400).astype(np.float32)
     np.testing.assert_array_equal(vals[rh['edge_id']][np.arange(r.nnz)], vals[rh['edge_id']])

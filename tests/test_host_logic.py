@@ -282,3 +282,21 @@ def test_auxiliary_dataset_restricts_and_renumbers():
     assert ident.train_data == DS.train_data
     empty = D.AuxiliaryDataset(DS(), {}, {})
     assert (empty.n_users, empty.n_items, empty.train_data, len(empty.train_pairs)) == (0, 0, [], 0)
+
+
+def test_utils_keeps_the_names_reference_code_imports():
+    """utils.py:280-305: AverageMeter and Unbuffered are imported by name by code written
+    against the reference."""
+    import io
+    from igr.utils import AverageMeter, Unbuffered
+    m = AverageMeter()
+    m.update(2.0, 3)
+    m.update(4.0, 1)
+    assert m.sum == 10.0 and m.count == 4 and m.avg == 2.5
+    buf = io.StringIO()
+    flushed = []
+    buf.flush = lambda: flushed.append(len(buf.getvalue()))
+    w = Unbuffered(buf)
+    w.write('ab')
+    w.writelines(['c', 'd'])
+    assert buf.getvalue() == 'abcd' and flushed == [2, 4] and w.closed is False

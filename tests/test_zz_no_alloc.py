@@ -49,7 +49,7 @@ def _both(g, v, x, epi_args=None):
     return outs
 
 
-@pytest.mark.parametrize('d', [64, 128, 48])
+@pytest.mark.parametrize('d', [64, 128, 32, 256])  # every width takes the chunk tier and its scratch
 def test_noalloc_matches_workspace_entry_point_twice(d):
     rng = np.random.default_rng(d)
     # first call: the larger graph; second call: a smaller one over the same array
@@ -80,3 +80,50 @@ def test_noalloc_rejects_oversized_scratch():
     assert b'IGR_SPMM_NOALLOC_MAX_FLOATS' in L.lib().igr_last_error()
     torch.cuda.synchronize()
     assert float(y.abs().sum()) == 0.0
+
+
+def test_noalloc_under_graph_capture_replays_match():
+    """The stated use: a captured hipGraph, which cannot allocate.  The first call is made
+    eagerly (it looks up the array's address), the second is captured, and three replays with
+    new inputs and eager work in between each equal igr_spmm_f32 bit for bit."""
+    d = 64
+    g, v = _graph(900, 700, 60000, 5)
+    vals = torch.from_numpy(v).to(DEV)
+    x = torch.randn(700, d, device=DEV)
+    y = torch.full((900, d), float('nan'), device=DEV)
+
+    def call():
+        L.call('igr_spmm_noalloc_f32', ctypes.byref(g.csr), d, x.data_ptr(), x.stride(0), vals.data_ptr(),
+               y.data_ptr(), y.stride(0), None, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    call()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            call()
+    torch.cuda.current_stream().wait_stream(side)
+    ws = torch.empty(g.n_chunks * d, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    for rep in range(3):
+        x.copy_(torch.randn(700, d, device=DEV, generator=gen))
+        y.fill_(float('nan'))
+        graph.replay()
+        torch.cuda.synchronize()
+        ref = torch.empty_like(y)
+        L.call('igr_spmm_f32', ctypes.byref(g.csr), d, x.data_ptr(), x.stride(0), vals.data_ptr(), ref.data_ptr(),
+               ref.stride(0), None, ws.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        assert torch.equal(y, ref), f'replay {rep}'
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason='needs two GPUs')
+def test_noalloc_rejects_an_output_on_another_device():
+    g, v = _graph(300, 200, 9000, 3)
+    d = 64
+    x = torch.zeros(200, d, device='cuda:1')
+    y = torch.zeros(300, d, device='cuda:1')
+    with torch.cuda.device(0):
+        rc = L.lib().igr_spmm_noalloc_f32(ctypes.byref(g.csr), d, x.data_ptr(), d, None, y.data_ptr(), d, None, None)
+    assert rc == 1 and b'is current' in L.lib().igr_last_error()

@@ -161,20 +161,25 @@ class BipartiteShard:
         return self._item_host
 
     @classmethod
-    def from_stream(cls, users, items, n_users, n_items, rank, world, device, group=None, timings=None, **kw):
+    def from_stream(cls, users, items, n_users, n_items, rank, world, device, group=None, timings=None,
+                    reduce=None, **kw):
         """A shard built from an interaction stream every rank holds (drawn from one
         seed, or read from one file) with the counting and the CSR builds divided
         among the ranks: rank k counts the degrees of the k-th slice of the stream,
         the counts are added up across the ranks (one host all-reduce of
         n_users + n_items integers), and each rank then selects and sorts only the
         interactions of its own user range.  Needs an initialised process group
-        when world > 1.  timings: dict that receives the seconds of each stage."""
+        when world > 1, unless `reduce` (counts of this rank's slice -> counts of the
+        whole stream) is given in place of the all-reduce.  timings: dict that
+        receives the seconds of each stage."""
         import time
         t0 = time.perf_counter()
         E = len(users)
         e0, e1 = E * rank // world, E * (rank + 1) // world
         counts = np.concatenate([count_ids(users[e0:e1], n_users), count_ids(items[e0:e1], n_items)])
-        if world > 1:
+        if reduce is not None:
+            counts = reduce(counts)
+        elif world > 1:
             counts = comm.all_reduce_sum_host(counts, group, device)
         degree = counts.astype(np.float32)
         t1 = time.perf_counter()

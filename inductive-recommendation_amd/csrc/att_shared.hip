@@ -62,6 +62,29 @@ __device__ __forceinline__ float group_sum(float x) {
     return x;
 }
 
+// Four per-lane partial sums (one per head) over the LPE lanes of a group, reduced so that
+// each lane ends with the FULL sum of ONE head instead of every lane with all four: a
+// butterfly - lanes of a pair exchange the two heads the other one keeps (xor 1), then the
+// one (xor 2), then the single value is added across the quads (mirrored halves, shuffles
+// beyond a 16-lane row).  Lane `sub` of the group ends with head head4_of(sub).  Odd quads
+// hold the heads in reverse order, so that a lane's partner under a row mirror (i <-> 7 - i,
+// i <-> 15 - i) holds the same head.  11 lane operations instead of 16, and the result is
+// laid out for one coalesced 4-byte store per lane.
+__device__ __forceinline__ int head4_of(int sub) { return (sub & 3) ^ ((sub & 4) ? 3 : 0); }
+
+template <int LPE>
+__device__ __forceinline__ float group_sum_heads4(float s0, float s1, float s2, float s3, bool b0, bool b1) {
+    static_assert(LPE >= 8, "a group spans at least two quads");
+    const float k01 = (b0 ? s1 : s0) + dpp_f<0xB1>(b0 ? s0 : s1);  // head b0
+    const float k23 = (b0 ? s3 : s2) + dpp_f<0xB1>(b0 ? s2 : s3);  // head 2 + b0
+    float x = (b1 ? k23 : k01) + dpp_f<0x4E>(b1 ? k01 : k23);     // head 2 b1 + b0, over the quad
+    x += dpp_f<0x141>(x);                 // row_half_mirror: the other quad of the 8
+    if (LPE >= 16) x += dpp_f<0x140>(x);  // row_mirror: the other 8 of the 16
+    if (LPE >= 32) x += shfl_xor_f(x, 16);
+    if (LPE >= 64) x += shfl_xor_f(x, 32);
+    return x;
+}
+
 template <int D, int H, bool EID>
 struct SddmmShared {
     static constexpr int LPE = D / 4;    // lanes per edge (source row)
@@ -69,6 +92,53 @@ struct SddmmShared {
     static constexpr int UE = IGR_SDDMM_SHARED_U > 0 ? IGR_SDDMM_SHARED_U : (16 / EPW < 1 ? 1 : (16 / EPW > 4 ? 4 : 16 / EPW));
     static constexpr int TRIP = UE * EPW;  // edges per trip (divides 64)
     static constexpr int NT = IGR_SDDMM_SHARED_NT < 64 / TRIP ? IGR_SDDMM_SHARED_NT : 64 / TRIP;  // trips per pass
+
+    // H = 4, one edge per group and trip: the butterfly leaves lane `sub` of group eg with one
+    // head of the trip's edge; the lanes whose quad index (sub >> 2) equals the trip's index
+    // inside a run of QT = LPE / 4 trips keep it, so after QT trips the 64 lanes hold the
+    // QT * EPW * 4 = 64 scores of QT * EPW consecutive edges - one 256-byte run of `out`,
+    // written by ONE store with every lane active (the per-edge 16-byte stores of one lane
+    // in sixteen cost 3.8 of 19.8 ms at nnz 411 M: 6.6 GB of scores at 1.7 TB/s).
+    template <int NTR>
+    static __device__ __forceinline__ void pass_heads4(int t0, int n, int cl, int eg, int sub, const v4f (&uq)[H],
+                                                       const float *__restrict__ vs, int ld_v,
+                                                       const int64_t *__restrict__ eid, int64_t base,
+                                                       float *__restrict__ out) {
+        constexpr int QT = LPE / 4;                    // trips per store
+        constexpr int NS = (NTR + QT - 1) / QT;        // stores of this pass
+        const bool odd = (sub & 4) != 0;
+        const bool b0 = ((sub & 1) != 0) != odd, b1 = ((sub & 2) != 0) != odd;
+        const int quad = sub >> 2;
+        v4f vk[NTR];
+#pragma unroll
+        for (int tt = 0; tt < NTR; ++tt) {
+            const int k = t0 + tt * EPW + eg;
+            const int c = shfl_i(cl, k < n ? k : n - 1);
+            vk[tt] = *reinterpret_cast<const v4f *>(vs + (int64_t)c * ld_v);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        float keep[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) keep[q] = 0.f;
+#pragma unroll
+        for (int tt = 0; tt < NTR; ++tt) {
+            float s[4];
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh)
+                s[hh] = uq[hh].x * vk[tt].x + uq[hh].y * vk[tt].y + uq[hh].z * vk[tt].z + uq[hh].w * vk[tt].w;
+            const float x = group_sum_heads4<LPE>(s[0], s[1], s[2], s[3], b0, b1);
+            if (quad == tt % QT) keep[tt / QT] = x;
+        }
+        const int hd = (b1 ? 2 : 0) + (b0 ? 1 : 0);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int k = t0 + (q * QT + quad) * EPW + eg;  // the edge whose score this lane kept
+            // q QT + quad < NTR: the lane kept a trip of THIS pass (a wide group has more quads than trips)
+            if (q * QT + quad < NTR && k < n) {
+                out[(EID ? eid[base + k] : base + k) * 4 + hd] = keep[q];
+            }
+        }
+    }
 
     // NTR trips starting at edge t0 of the block: every gather first, then each trip's
     // dots, their sums over the group's lanes and the stores (lane 0 of the group
@@ -78,6 +148,10 @@ struct SddmmShared {
                                                 const float *__restrict__ vs, int ld_v,
                                                 const int64_t *__restrict__ eid, int64_t base,
                                                 float *__restrict__ out) {
+        if constexpr (H == 4 && UE == 1 && LPE >= 8) {
+            pass_heads4<NTR>(t0, n, cl, eg, sub, uq, vs, ld_v, eid, base, out);
+            return;
+        }
         v4f vk[NTR][UE];
 #pragma unroll
         for (int tt = 0; tt < NTR; ++tt)
@@ -118,6 +192,9 @@ struct SddmmShared {
     }
 };
 
+constexpr int kXcds = 8;
+constexpr int kXcdStrip = 32;  // workgroups (128 rows) per strip
+
 template <int D, int H, bool EID, bool PLAN>
 __global__ __launch_bounds__(256) void sddmm_shared_kernel(int64_t n_rows, const int64_t *__restrict__ row_ptr,
                                                            const int32_t *__restrict__ col,
@@ -126,7 +203,20 @@ __global__ __launch_bounds__(256) void sddmm_shared_kernel(int64_t n_rows, const
                                                            const float *__restrict__ v, int ld_v,
                                                            float *__restrict__ out) {
     using S = SddmmShared<D, H, EID>;
-    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (!PLAN) {
+        // natural row order: workgroups are dealt to the 8 XCDs round-robin, so they are
+        // renumbered for each XCD to walk strips of kXcdStrip consecutive workgroups' rows
+        // (the grid is a whole number of 8-strip groups).  The scores of neighbouring rows
+        // share 128-byte lines, and a line written half through one XCD's L2 and half
+        // through another's reaches memory twice.  Strips, not one range per XCD: the
+        // heavy rows of a bipartite graph sit together (the item rows: half of the edges in
+        // a tenth of the rows), and the XCD that owned them all would finish 2.6 times later.
+        const int64_t q = blockIdx.x / kXcds;
+        const int64_t lb = (q / kXcdStrip) * (kXcds * kXcdStrip) + (int64_t)(blockIdx.x % kXcds) * kXcdStrip +
+                           q % kXcdStrip;
+        w = lb * 4 + (threadIdx.x >> 6);
+    }
     int64_t r, b, e;
     if (PLAN) {
         if (w >= plan.n_chunks + plan.n_order) return;
@@ -335,7 +425,12 @@ struct LaunchSddmmShared {
         const RowPlan plan = row_plan_of(g);
         const bool planned = use_row_plan(g);
         const int64_t waves = planned ? g->n_chunks + g->n_order : g->n_rows;
-        const dim3 grid((unsigned)((waves + 3) / 4));
+        int64_t blocks = (waves + 3) / 4;
+        if (!planned) {  // whole groups of 8 strips: every renumbered workgroup below the count is taken
+            const int64_t group = (int64_t)kXcds * kXcdStrip;
+            blocks = (blocks + group - 1) / group * group;
+        }
+        const dim3 grid((unsigned)blocks);
 #define IGR_GO(EID_, PLAN_)                                                                                    \
     hipLaunchKernelGGL((sddmm_shared_kernel<D, H, EID_, PLAN_>), grid, dim3(256), 0, st, g->n_rows, g->row_ptr, \
                        g->col_idx, g->edge_id, plan, u, ld_u, v, (int)ld_v, out)

@@ -146,6 +146,9 @@ __device__ __forceinline__ float uniform24(uint64_t seed, uint64_t offset, uint6
 
 // Lane shuffle within the wave (ds_bpermute).
 __device__ __forceinline__ int shfl_i(int v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ int64_t shfl_i64(int64_t v, int src) {
+    return ((int64_t)__shfl((int)(v >> 32), src, 64) << 32) | (uint32_t)__shfl((int)v, src, 64);
+}
 __device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src, 64); }
 __device__ __forceinline__ float shfl_xor_f(float v, int m) { return __shfl_xor(v, m, 64); }
 

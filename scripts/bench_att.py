@@ -97,6 +97,18 @@ def main():
     byts = g.nnz * (8 + 4 * d) + g.n_rows * (8 + 4 * d)
     res['spmm_att'] = {'ms': ms, 'edges_per_s': g.nnz / ms * 1e3, 'algorithmic_GBps': byts / ms / 1e6,
                        'frac': byts / ms / 1e6 / 8000.0}
+    # its gradient with respect to E: the reverse-graph SpMM with the same per-edge weights, which
+    # the reverse graph addresses through its edge ids - read in place (eid), or permuted once
+    # into the reverse graph's order (perm) and then streamed (pos)
+    rev = g.reverse()
+    dy = torch.randn(g.n_rows, d, device=dev, generator=gen) * 0.1
+    dx = torch.empty(g.n_cols, d, device=dev)
+    ms_eid = timed(lambda: ops.spmm(rev, dy, w, out=dx), args.steps, args.warmup)
+    ms_perm = timed(lambda: holder.__setitem__('p', w[rev.edge_id]), args.steps, args.warmup)
+    ms_pos = timed(lambda: ops.spmm(rev.positional(), dy, holder['p'], out=dx), args.steps, args.warmup)
+    res['spmm_att_bwd'] = {'ms_values_by_edge_id': ms_eid, 'ms_permute_values': ms_perm, 'ms_positional': ms_pos,
+                           'frac_by_edge_id': byts / ms_eid / 1e6 / 8000.0,
+                           'frac_permute_plus_positional': byts / (ms_perm + ms_pos) / 1e6 / 8000.0}
     print(json.dumps({'graph': 'IGCN feature graph (feature_ratio 1)', 'n_users': U, 'n_items': I,
                       'n_draws': args.n_edges, 'nnz': g.nnz, 'd': d, 'heads': H, 'launches': res}))
 

@@ -972,6 +972,49 @@ def test_sddmm_shared_source_and_its_gradient(h, d, dedup):
     assert torch.equal(ut.grad, y)
 
 
+@pytest.mark.parametrize('h,d,dedup', [(4, 64, True), (1, 64, False), (2, 128, True), (8, 32, True)])
+def test_sddmm_shared_source_on_a_graph_without_row_plan(h, d, dedup):
+    """The same scores on a graph too large for the row plan and without split rows (more than
+    2^18 rows, none above the split threshold): rows in natural order with the workgroups
+    renumbered in strips per XCD (the grid is padded to whole groups of strips, so the last
+    group is partly empty); runs of empty rows, rows of exactly 64 and 65 edges, rows of
+    several blocks, short tails (the one-store-per-16-edges layout); multigraph edge ids."""
+    n_rows, n_cols = 300_011, 5000
+    rng = np.random.default_rng(h + d)
+    deg = rng.integers(0, 9, n_rows)
+    deg[1000:1100] = 0              # more empty rows than a wave walks
+    deg[5] = 64
+    deg[6] = 65
+    deg[7] = 0
+    deg[8] = 300
+    deg[n_rows - 1] = 130
+    deg[n_rows - 2] = 0
+    row = np.repeat(np.arange(n_rows), deg)
+    col = rng.integers(0, n_cols, len(row))
+    if not dedup:  # an unsorted multigraph edge list: edge ids differ from CSR positions
+        perm = rng.permutation(len(row))
+        row, col = row[perm], col[perm]
+    g, _ = G.Graph.from_coo(row, col, n_rows, n_cols, None, dedup=dedup, device=DEV, split_threshold=512,
+                            chunk_edges=512)  # the plan of a large graph: no row of this one is split
+    assert g.n_chunks == 0 and g.n_rows > (1 << 18)
+    u = (rng.standard_normal((n_rows, h * d)) * 0.5).astype(np.float32)
+    v = rng.standard_normal((n_cols, d)).astype(np.float32)
+    out = torch.full((g.nnz, h), float('nan'), device=DEV)
+    ops.sddmm_shared(g, t(u), t(v), h, out=out)
+    assert not torch.isnan(out).any()
+    hst = g.host()
+    r_e = np.repeat(np.arange(n_rows), np.diff(hst['row_ptr']))
+    c_e = hst['col_idx'].astype(np.int64)
+    eid = hst['edge_id'] if hst['edge_id'] is not None else np.arange(g.nnz)
+    assert dedup or hst['edge_id'] is not None
+    u64, v64 = u.astype(np.float64).reshape(n_rows, h, d), v.astype(np.float64)
+    ref, mag = np.empty((g.nnz, h)), np.empty((g.nnz, h))
+    ref[eid] = np.einsum('ehk,ek->eh', u64[r_e], v64[c_e])
+    mag[eid] = np.einsum('ehk,ek->eh', np.abs(u64[r_e]), np.abs(v64[c_e]))
+    assert np.all(np.abs(out.cpu().numpy() - ref) <= d * 2.0 ** -24 * mag + 1e-30)
+    assert torch.equal(out, ops.sddmm_shared(g, t(u), t(v), h))
+
+
 @pytest.mark.parametrize('n', [1, 7, 1024, 2048, 5001])
 def test_means_of_loss_terms(n):
     """mean(a), mean(b) in one launch: against float64, equal on repeated calls, b optional."""

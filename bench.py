@@ -145,6 +145,9 @@ def main():
     ap.add_argument('--replicate', default='auto', choices=['auto', 'items', 'users'],
                     help='side replicated on every rank (auto: the smaller one); the other is cut into ranges')
     ap.add_argument('--dist-backend', default='nccl', help="'nccl' (= RCCL on ROCm); 'gloo' only for rehearsals")
+    ap.add_argument('--dist-at-world-1', action='store_true',
+                    help='with one rank: still create the process group and run the exchange and every reduce '
+                         'of the multi-rank code through it (checks the RCCL path on a one-GPU box)')
     ap.add_argument('--one-device', action='store_true',
                     help='map every rank to cuda:0 (multi-rank rehearsal on a one-GPU box, with --dist-backend gloo)')
     args = ap.parse_args()
@@ -161,7 +164,13 @@ def main():
     dev_index = 0 if args.one_device else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device('cuda', dev_index)
-    if world > 1:
+    multi = world > 1 or args.dist_at_world_1  # the process group exists and the exchange runs
+    if multi:
+        if world == 1:  # no launcher set the rendezvous up
+            os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+            os.environ.setdefault('MASTER_PORT', str(29500 + os.getpid() % 2000))
+            os.environ.setdefault('RANK', '0')
+            os.environ.setdefault('WORLD_SIZE', '1')
         if args.dist_backend == 'nccl':
             # RCCL over xGMI; its stream stays at the default priority (streams of
             # different priorities have hung on these machines)
@@ -169,7 +178,7 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    from igr import ops
+    from igr import comm, ops  # noqa: F401
     from igr.dataset import synthetic_pairs
     from igr.dist import BipartiteShard, sharded_side
 
@@ -184,7 +193,10 @@ def main():
     setup = {'draw_s': time.time() - t0}
     log(f'building shard (C++ CSR build; {side} sharded) ... {time.time() - t0:.1f}s')
     shard = BipartiteShard.from_stream(su, si, SU, SI, rank, world, dev, timings=setup, d=d,
-                                       item_tiles=args.item_tiles)
+                                       item_tiles=args.item_tiles,
+                                       reduce=(lambda c: comm.all_reduce_sum_host(c, None, dev)) if multi else None,
+                                       **({'item_chunks': 4} if multi else {}))
+    shard.exchange = multi
     del su, si
     setup['total_s'] = time.time() - t0
     nu = shard.u1 - shard.u0
@@ -240,7 +252,7 @@ def main():
     nl = len(launches)
     ev = [[[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(nl)] for _ in range(args.steps)]
     ev_done = torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
@@ -248,7 +260,7 @@ def main():
         step(ev[s])
     drain(ev_done)
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     kern_ms = np.array([[ev[s][k][0].elapsed_time(ev[s][k][1]) for k in range(nl)] for s in range(args.steps)])
@@ -260,7 +272,7 @@ def main():
     exposed_ms += ev[-1][nl - 1][1].elapsed_time(ev_done) / args.steps
     compute_ms = float(kern_ms.sum(1).mean())
 
-    if world > 1:
+    if multi:
         # RCCL reduces device tensors; a gloo rehearsal is only ever handed CPU tensors
         sdev = dev if args.dist_backend == 'nccl' else torch.device('cpu')
         t = torch.tensor([elapsed], dtype=torch.float64, device=sdev)
@@ -353,7 +365,7 @@ def main():
                                  'all-reduces before its user-side SpMM, plus the final wait (0 at N = 1)'},
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 

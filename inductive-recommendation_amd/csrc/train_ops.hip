@@ -243,30 +243,13 @@ extern "C" int igr_adam_f32(int64_t n, float *param, const float *grad, float *e
         const float bc2_sqrt = (float)std::sqrt(bc2);
         hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         const float omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2);
-        // one float4 of each array per thread (no grid cap) with non-temporal
-        // traffic: 5.15 -> 5.7 TB/s on the 70 M-parameter table
-        // (scripts/tune_adam.py, profiles/r01m_adam_sweep.json); the knobs
-        // IGR_ADAM_U (float4s per thread per trip), IGR_ADAM_GRID (> 0: cap)
-        // and IGR_ADAM_NT are read per call for that sweep
-        const char *eu = getenv("IGR_ADAM_U");
-        const char *eg = getenv("IGR_ADAM_GRID");
-        const char *en = getenv("IGR_ADAM_NT");
-        const int U = eu ? atoi(eu) : 1;
-        const bool nt = en ? atoi(en) == 1 : true;
-        int64_t grid = std::min<int64_t>(((n + 3) / 4 + 255) / 256, int64_t(1) << 30);
-        if (eg && atoi(eg) > 0) grid = std::min<int64_t>(grid, atoi(eg));
-        grid = std::max<int64_t>(grid, 1);
-#define IGR_ADAM(UU)                                                                                             \
-    if (nt) hipLaunchKernelGGL((adam_kernel<UU, true>), dim3((unsigned)grid), dim3(256), 0, st, n, param, grad,      \
-                               exp_avg, exp_avg_sq, omb1, (float)beta2, omb2, (float)eps, (float)weight_decay,      \
-                               step_size, bc2_sqrt, step_dev, step, lr, beta1, beta2);                               \
-    else hipLaunchKernelGGL((adam_kernel<UU, false>), dim3((unsigned)grid), dim3(256), 0, st, n, param, grad, exp_avg, exp_avg_sq, \
-                       omb1, (float)beta2, omb2, (float)eps, (float)weight_decay, step_size, bc2_sqrt, step_dev, step,  \
-                       lr, beta1, beta2)
-        if (U == 4) IGR_ADAM(4);
-        else if (U == 2) IGR_ADAM(2);
-        else IGR_ADAM(1);
-#undef IGR_ADAM
+        // one float4 of each array per thread, no grid cap, non-temporal traffic: the best of
+        // the sweep over float4s per thread x grid cap x temporal hint on the 70 M-parameter
+        // table (5.15 -> 5.7 TB/s, profiles/r01m_adam_sweep.json); the wider variants spilled
+        const int64_t grid = std::max<int64_t>(std::min<int64_t>(((n + 3) / 4 + 255) / 256, int64_t(1) << 30), 1);
+        hipLaunchKernelGGL((adam_kernel<1, true>), dim3((unsigned)grid), dim3(256), 0, st, n, param, grad, exp_avg,
+                           exp_avg_sq, omb1, (float)beta2, omb2, (float)eps, (float)weight_decay, step_size, bc2_sqrt,
+                           step_dev, step, lr, beta1, beta2);
         return launch_status("igr_adam_f32");
     });
 }

@@ -34,6 +34,9 @@ def main():
     ap.add_argument('--l2-reg', type=float, default=0., help='trainer l2_reg (0 skips the l2 term, as the IGCN configs do)')
     ap.add_argument('--eval', action='store_true', help='also time one full eval ranking (Recall@20 path)')
     ap.add_argument('--graph', action='store_true', help='replay one hipGraph-captured step (trainer.StepGraph)')
+    ap.add_argument('--epochs', type=int, default=0,
+                    help='time this many train_one_epoch() calls of the trainer as configured by default (no '
+                         "'graph' key: the trainer picks the captured step where it applies) instead of single steps")
     ap.add_argument('--dist-backend', default='nccl', help="'nccl' (= RCCL); 'gloo' for rehearsals (host-staged)")
     ap.add_argument('--one-device', action='store_true',
                     help='every rank on cuda:0 (multi-rank rehearsal on a one-GPU box, with --dist-backend gloo)')
@@ -120,6 +123,21 @@ def main():
             return tr.step(u, p, n)
         au, ap_, an = tr.aux_sampler.sample(args.batch)
         return tr.step(u, p, n, au, ap_, an)
+    if args.epochs:
+        steps = len(tr.sampler)
+        tr.train_one_epoch()  # builds the captured step (or not) and warms up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.epochs):
+            loss = tr.train_one_epoch()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        print(json.dumps({'model': args.model, 'mode': 'train_one_epoch, default trainer config',
+                          'captured_step': bool(T.graph_mode_for(tr)), 'steps_per_epoch': steps, 'epochs': args.epochs,
+                          'epoch_s': el / args.epochs, 'ms_per_step': el / args.epochs / steps * 1e3, 'loss': float(loss),
+                          'n_users': args.n_users, 'n_items': args.n_items, 'n_edges': args.n_edges, 'd': args.d,
+                          'layers': args.layers}))
+        return
     if args.graph:
         sg = T.StepGraph(tr, args.batch)
 

@@ -88,10 +88,11 @@ def test_real_ranks_see_their_environment_and_failures_propagate(tmp_path, fail_
 
 
 def test_bench_starts_its_own_ranks_before_any_gpu_call():
-    """`python bench.py --gpus 8` on a machine without 8 GPUs: refused by the launcher with
-    a message (exit code 2), not an assertion from a rank that was never started."""
+    """`python bench.py --gpus N` on a machine without N GPUs (N = 1000: no node has that many, so
+    this never starts a real run): refused by the launcher with a message (exit code 2), not an
+    assertion from a rank that was never started."""
     env = {k: v for k, v in os.environ.items() if k not in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK')}
-    r = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '8'], capture_output=True,
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '1000'], capture_output=True,
                        text=True, env=env, timeout=300)
     assert r.returncode == 2 and 'GPU(s) visible' in r.stderr and 'AssertionError' not in r.stderr
 

@@ -13,7 +13,7 @@ B=$ROOT/inductive-recommendation_amd/build/sanitize
 CSRC=$ROOT/inductive-recommendation_amd/csrc
 mkdir -p "$B" "$OUT"
 INC="-I$ROOT/include -I$CSRC -I/opt/rocm/include -D__HIP_PLATFORM_AMD__"
-LOG=$OUT/r02_sanitize_host.txt
+LOG=$OUT/${SAN_TAG:-r03}_sanitize_host.txt
 : > "$LOG"
 for san in address,undefined thread; do
   tag=${san//,/_}
@@ -25,7 +25,7 @@ for san in address,undefined thread; do
       "./driver_$tag" ) 2>&1 | tee -a "$LOG"
 done
 echo "== hipcc, host pass with -fsanitize=address,undefined: whole library + Python host tests" | tee -a "$LOG"
-SRCS="spmm.hip spmm_rows.hip topk.hip edge_ops.hip att_shared.hip bpr.hip rowsort.hip gemm.hip train_ops.hip graph_host.cpp capi.cpp"
+SRCS="spmm.hip spmm_rows.hip topk.hip edge_ops.hip att_shared.hip bpr.hip rowsort.hip gemm.hip linear_wgrad.hip train_ops.hip graph_host.cpp capi.cpp"
 OBJS=""
 for s in $SRCS; do
   o=$B/${s%.*}.o

@@ -128,6 +128,32 @@ static void one_case(int64_t nr, int64_t nc, int64_t n, unsigned seed) {
         }
         for (int64_t row = 0; row < nr; ++row) CHECK(seen[row] == 1);
     }
+    // the shard set-up passes: occurrences of each id, and the pairs of one id range in stream order
+    for (int nt : {1, 8}) {
+        std::vector<int64_t> cnt(nr, -1), ref(nr, 0);
+        CHECK(igr_count_ids(n, r.data(), nr, cnt.data(), nt) == 0);
+        for (int64_t i = 0; i < n; ++i) ref[r[i]]++;
+        CHECK(cnt == ref);
+        const int64_t lo = nr / 4, hi = nr / 4 + std::max<int64_t>(1, nr / 2);
+        int64_t m = -1;
+        CHECK(igr_select_id_range(n, r.data(), c.data(), lo, hi, nullptr, nullptr, &m, nt) == 0);
+        std::vector<int64_t> ok(std::max<int64_t>(m, 1)), oo(std::max<int64_t>(m, 1));
+        int64_t m2 = -1;
+        CHECK(igr_select_id_range(n, r.data(), c.data(), lo, hi, ok.data(), oo.data(), &m2, nt) == 0);
+        CHECK(m2 == m);
+        int64_t j = 0;
+        for (int64_t i = 0; i < n; ++i)
+            if (r[i] >= lo && r[i] < hi) {
+                CHECK(j < m && ok[j] == r[i] - lo && oo[j] == c[i]);
+                ++j;
+            }
+        CHECK(j == m);
+    }
+    {
+        std::vector<int64_t> bad = r, cnt(nr);
+        bad[n - 1] = nr;
+        CHECK(igr_count_ids(n, bad.data(), nr, cnt.data(), 8) == IGR_ERR_ARG);
+    }
     // error path: an out-of-range index is refused with a message
     std::vector<int64_t> rb = r, rp(nr + 1);
     std::vector<int32_t> cb(n);

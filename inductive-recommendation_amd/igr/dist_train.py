@@ -40,7 +40,7 @@ import torch.nn as nn
 
 from . import comm, ops
 from .dist import BipartiteShard, _hip_spmm
-from .graph import Graph, csr_from_coo
+from .graph import Graph, count_ids, csr_from_coo, select_id_range
 from .model import train_pairs
 
 
@@ -57,12 +57,14 @@ class FeatureShard:
     reference's feature matrix (duplicates counted, + 1 for the general
     feature), so the values equal the unsharded model's."""
 
-    def __init__(self, pairs, n_users, n_items, u0, u1, rank, device):
+    def __init__(self, pairs, n_users, n_items, u0, u1, rank, device, degree=None):
+        """degree: float32 [U + I] interaction counts of the WHOLE graph when the caller has
+        them already (BipartiteShard.degree: counted once, by all ranks together); counted here
+        otherwise."""
         U, I = n_users, n_items
         nk = u1 - u0
         u, i = pairs[:, 0], pairs[:, 1]
-        mine = (u >= u0) & (u < u1)
-        lu, li = u[mine] - u0, i[mine]
+        lu, li = select_id_range(u, i, u0, u1)
         rows = [lu, nk + li, np.arange(nk)]
         cols = [nk + li, lu, np.full(nk, nk + I)]
         if rank == 0:  # the general item feature enters the item rows' sum once
@@ -71,8 +73,10 @@ class FeatureShard:
         rp, ci, _, _ = csr_from_coo(np.concatenate(rows), np.concatenate(cols), nk + I, nk + I + 2, None,
                                     dedup=True, want_eid=False)
         self.graph = Graph(rp, ci, nk + I, nk + I + 2, device=device)
-        deg_u = np.bincount(u, minlength=U).astype(np.float32)
-        deg_i = np.bincount(i, minlength=I).astype(np.float32)
+        if degree is None:
+            deg_u, deg_i = count_ids(u, U).astype(np.float32), count_ids(i, I).astype(np.float32)
+        else:
+            deg_u, deg_i = degree[:U], degree[U:]
         self.row_sum = torch.from_numpy(np.concatenate([deg_u[u0:u1], deg_i]) + np.float32(1.)).to(device)
         self.n_local, self.n_items = nk, I
 
@@ -334,9 +338,13 @@ class ShardedIGCN(nn.Module):
         # last layer only at the batch rows (ShardedPropagateRows); 'batch_rep' False = full layers
         self.batch_rows = bool(model_config.get('batch_rep', True)) and self.n_layers > 0
         pairs = train_pairs(ds)
-        self.shard = BipartiteShard(pairs, self.n_users, self.n_items, rank, world, self.device, d=d)
+        # set-up divided among the ranks: each counts one slice of the pairs, one host all-reduce
+        # of the degrees, then every rank sorts only its own users' interactions
+        self.shard = BipartiteShard.from_stream(pairs[:, 0], pairs[:, 1], self.n_users, self.n_items, rank, world,
+                                                self.device, group=group, d=d)
         self.u0, self.u1 = self.shard.u0, self.shard.u1
-        self.feat = FeatureShard(pairs, self.n_users, self.n_items, self.u0, self.u1, rank, self.device)
+        self.feat = FeatureShard(pairs, self.n_users, self.n_items, self.u0, self.u1, rank, self.device,
+                                 degree=self.shard.degree)
         self.n_local = self.u1 - self.u0
         self.embedding = nn.Embedding(self.feat.graph.n_cols, d)
         nn.init.normal_(self.embedding.weight, std=0.1)  # model.py:4124

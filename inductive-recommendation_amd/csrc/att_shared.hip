@@ -97,8 +97,9 @@ struct SddmmShared {
     // head of the trip's edge; the lanes whose quad index (sub >> 2) equals the trip's index
     // inside a run of QT = LPE / 4 trips keep it, so after QT trips the 64 lanes hold the
     // QT * EPW * 4 = 64 scores of QT * EPW consecutive edges - one 256-byte run of `out`,
-    // written by ONE store with every lane active (the per-edge 16-byte stores of one lane
-    // in sixteen cost 3.8 of 19.8 ms at nnz 411 M: 6.6 GB of scores at 1.7 TB/s).
+    // written by ONE store with every lane active instead of four 16-byte stores from one
+    // lane in sixteen (19.8 -> 19.1 ms at nnz 411 M, h = 4, d = 64; the launch takes 16.0 ms
+    // with no stores at all, so most of what the 6.6 GB of scores cost is not their shape).
     template <int NTR>
     static __device__ __forceinline__ void pass_heads4(int t0, int n, int cl, int eg, int sub, const v4f (&uq)[H],
                                                        const float *__restrict__ vs, int ld_v,
@@ -106,8 +107,8 @@ struct SddmmShared {
                                                        float *__restrict__ out) {
         constexpr int QT = LPE / 4;                    // trips per store
         constexpr int NS = (NTR + QT - 1) / QT;        // stores of this pass
-        const bool odd = (sub & 4) != 0;
-        const bool b0 = ((sub & 1) != 0) != odd, b1 = ((sub & 2) != 0) != odd;
+        const int hd = head4_of(sub);  // the head this lane ends up holding
+        const bool b0 = (hd & 1) != 0, b1 = (hd & 2) != 0;
         const int quad = sub >> 2;
         v4f vk[NTR];
 #pragma unroll
@@ -129,7 +130,6 @@ struct SddmmShared {
             const float x = group_sum_heads4<LPE>(s[0], s[1], s[2], s[3], b0, b1);
             if (quad == tt % QT) keep[tt / QT] = x;
         }
-        const int hd = (b1 ? 2 : 0) + (b0 ? 1 : 0);
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
             const int k = t0 + (q * QT + quad) * EPW + eg;  // the edge whose score this lane kept

@@ -1,0 +1,106 @@
+"""The sharded layer's ordering against a collective that really is asynchronous.
+
+A one-rank RCCL all-reduce moves no data and gloo's staged path is synchronous, so neither
+shows a missing stream dependency.  Here the exchange is replaced by a stand-in with the
+stream semantics torch gives an RCCL collective - it runs on a stream of its own, which first
+waits for the work already queued on the caller's stream; `wait()` makes the caller's stream
+wait for it - that is slow (it spins for milliseconds before touching the data) and that
+changes the data the way a second, identical rank would: partial sums are doubled.  Every
+layer's result is then known exactly (doubling is exact in fp32):
+
+    items' output = 2 x (A_iu x_u),   users' output = A_ui x_i   with x_i the doubled items
+
+and any read before the exchange has finished, or an exchange started before its SpMM has
+written, shows up as a wrong number.  The same stand-in with `wait()` switched off must give
+different numbers: the check that the test can see a missing wait at all.
+"""
+import numpy as np
+import pytest
+import torch
+
+from igr import comm, dist
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda')
+SPIN = 20_000_000  # cycles the stand-in collective spins before it touches the data (milliseconds)
+
+
+class _Work:
+    def __init__(self, done, honour_wait):
+        self.done, self.honour_wait = done, honour_wait
+
+    def wait(self):
+        if self.honour_wait:
+            torch.cuda.current_stream().wait_event(self.done)
+        return True
+
+
+def _standin(side, honour_wait=True):
+    def all_reduce_sum(t, group=None, async_op=False):
+        cur = torch.cuda.current_stream()
+        ready = torch.cuda.Event()
+        ready.record(cur)                     # everything queued so far, the SpMM that wrote t included
+        with torch.cuda.stream(side):
+            side.wait_event(ready)
+            torch.cuda._sleep(SPIN)
+            t.mul_(2.0)                       # the sum over two identical ranks
+            done = torch.cuda.Event()
+            done.record(side)
+        w = _Work(done, honour_wait)
+        if async_op:
+            return w
+        w.wait()
+        return None
+    return all_reduce_sum
+
+
+def _shard(chunks, tiles):
+    rng = np.random.default_rng(2)
+    U, I, E = 50_000, 8_000, 600_000
+    sh = dist.BipartiteShard.from_stream(rng.integers(0, U, E), rng.integers(0, I, E), U, I, 0, 1, DEV,
+                                         item_chunks=chunks, item_tiles=tiles)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    return sh, torch.randn(U, 64, generator=g, device=DEV), torch.randn(I, 64, generator=g, device=DEV)
+
+
+def _expected(sh, xu, xi, layers):
+    """Chained layers with the items' output doubled after each one, no exchange involved."""
+    assert sh.exchange is False
+    for _ in range(layers):
+        yu, yi = sh.layer(xu, xi)
+        xu, xi = yu, yi * 2.0
+    torch.cuda.synchronize()
+    return xu, xi
+
+
+@pytest.mark.parametrize('chunks,tiles', [(4, 1), (2, 3)])
+def test_deferred_waits_order_the_layers_against_an_asynchronous_exchange(monkeypatch, chunks, tiles):
+    sh, xu, xi = _shard(chunks, tiles)
+    want_u, want_i = _expected(sh, xu, xi, 4)
+    side = torch.cuda.Stream()
+    monkeypatch.setattr(comm, 'all_reduce_sum', _standin(side))
+    sh.exchange = True
+    # chained layers, every wait deferred into the next layer (bench.py, propagate)
+    got_u, got_i = sh.propagate(xu, xi, 4)
+    torch.cuda.synchronize()
+    assert torch.equal(got_u, want_u) and torch.equal(got_i, want_i)
+    # single layers with the wait inside (dist_train), into fresh buffers and into the caller's
+    yu, yi = sh.layer(xu, xi)
+    torch.cuda.synchronize()
+    sh.exchange = False
+    pu, pi = sh.layer(xu, xi)
+    assert torch.equal(yu, pu) and torch.equal(yi, pi * 2.0)
+
+
+def test_a_missing_wait_is_visible_to_this_test(monkeypatch):
+    """Sensitivity: with wait() doing nothing the next layer reads the items before the
+    stand-in has doubled them, and the numbers differ."""
+    sh, xu, xi = _shard(4, 1)
+    want_u, want_i = _expected(sh, xu, xi, 3)
+    side = torch.cuda.Stream()
+    monkeypatch.setattr(comm, 'all_reduce_sum', _standin(side, honour_wait=False))
+    sh.exchange = True
+    got_u, got_i = sh.propagate(xu, xi, 3)
+    torch.cuda.synchronize()
+    side.synchronize()
+    assert not torch.equal(got_u, want_u)

@@ -164,6 +164,14 @@ def main():
     dev_index = 0 if args.one_device else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device('cuda', dev_index)
+    # host threads of this rank's set-up (the C++ graph builder reads IGR_NUM_THREADS first):
+    # a launcher that finds OMP_NUM_THREADS unset gives every rank ONE thread, which would make
+    # the CSR builds of a 200 M-pair graph take minutes; a GPU's share of the host is 16 cores
+    # here, and ranks rehearsing on one GPU box share that one share
+    local_world = int(os.environ.get('LOCAL_WORLD_SIZE', world))
+    share = 16 // local_world if args.one_device else min(16, len(os.sched_getaffinity(0)) // max(1, local_world))
+    os.environ.setdefault('IGR_NUM_THREADS', str(max(1, share)))
+    torch.set_num_threads(int(os.environ['IGR_NUM_THREADS']))  # torch's own host passes (gathers) likewise
     multi = world > 1 or args.dist_at_world_1  # the process group exists and the exchange runs
     if multi:
         if world == 1:  # no launcher set the rendezvous up

@@ -205,7 +205,7 @@ def sharded(args, ds, rank, world, dev):
     if rank == 0:
         print(json.dumps({'mode': 'sharded', 'world': world, 'backend': args.dist_backend,
                           'one_device': args.one_device, 'ms_per_step': el / args.steps * 1e3,
-                          'samples_per_s': world * args.batch * args.steps / el, 'loss': float(loss),
+                          'samples_per_s': world * args.batch * args.steps / el, 'loss': float(torch.as_tensor(loss).detach()),
                           'n_users': args.n_users, 'n_items': args.n_items, 'n_edges': args.n_edges, 'd': args.d,
                           'layers': args.layers}))
     if world > 1:

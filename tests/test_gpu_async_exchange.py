@@ -104,3 +104,47 @@ def test_a_missing_wait_is_visible_to_this_test(monkeypatch):
     torch.cuda.synchronize()
     side.synchronize()
     assert not torch.equal(got_u, want_u)
+
+
+def _sync_standin():
+    """The same arithmetic on the caller's own stream: ordered by construction."""
+    def all_reduce_sum(t, group=None, async_op=False):
+        t.mul_(2.0)
+        return comm._Done() if async_op else None
+    return all_reduce_sum
+
+
+@pytest.mark.parametrize('layers', [0, 1, 3])
+def test_sharded_igcn_forward_and_backward_are_ordered_against_an_asynchronous_exchange(monkeypatch, layers):
+    """igr.dist_train.ShardedPropagate (full-layer path): the inductive layer's item rows are
+    reduced while the first layer's item side runs, the layers' reduces are waited inside each
+    layer, the backward reduces the batch items first.  One rank made to behave as one of two
+    (model.world = 2, the exchange switched on); the run with the slow asynchronous stand-in must
+    equal, bit for bit, the run whose stand-in works on the caller's own stream - representation
+    and embedding gradient, in train mode (dropout drawn in the SpMM)."""
+    from igr.dist_train import ShardedIGCN
+    rng = np.random.default_rng(4)
+    U, I, E, d = 20_000, 3_000, 200_000, 64
+    pairs = np.stack([rng.integers(0, U, E), rng.integers(0, I, E)], 1)
+
+    class DS:
+        name, n_users, n_items, train_pairs = 'synthetic', U, I, pairs
+
+    def run(standin):
+        torch.manual_seed(0)
+        m = ShardedIGCN({'embedding_size': d, 'n_layers': layers, 'device': DEV, 'dropout': 0.3, 'feature_ratio': 1.,
+                         'dataset': DS(), 'batch_rep': False, 'seed': 5}, 0, 1)
+        m.world, m.shard.exchange = 2, True  # one of two identical ranks, as far as the exchange goes
+        monkeypatch.setattr(comm, 'all_reduce_sum', standin)
+        m.train()
+        rep = m.get_rep()
+        g = torch.Generator(device=DEV).manual_seed(1)
+        (rep * torch.randn(rep.shape, generator=g, device=DEV)).sum().backward()
+        torch.cuda.synchronize()
+        return rep.detach().clone(), m.embedding.weight.grad.detach().clone()
+
+    want_rep, want_grad = run(_sync_standin())
+    got_rep, got_grad = run(_standin(torch.cuda.Stream()))
+    assert float(want_rep.abs().sum()) > 0 and float(want_grad.abs().sum()) > 0
+    assert torch.equal(got_rep, want_rep)
+    assert torch.equal(got_grad, want_grad)

@@ -148,3 +148,41 @@ def test_sharded_igcn_forward_and_backward_are_ordered_against_an_asynchronous_e
     assert float(want_rep.abs().sum()) > 0 and float(want_grad.abs().sum()) > 0
     assert torch.equal(got_rep, want_rep)
     assert torch.equal(got_grad, want_grad)
+
+
+@pytest.mark.parametrize('batch_rep', [True, False])
+def test_sharded_training_steps_are_ordered_against_an_asynchronous_exchange(monkeypatch, batch_rep):
+    """Three whole steps of ShardedIGCNTrainer (batch-row path and full-layer path: forward,
+    backward, the gradient reduce, fused Adam) as one of two identical ranks - the all-gathers
+    hand back this rank's data twice, the all-reduces double - with the slow asynchronous
+    stand-in and with the one on the caller's own stream: every parameter bit for bit."""
+    from igr.dist_train import ShardedIGCN, ShardedIGCNTrainer
+    rng = np.random.default_rng(6)
+    U, I, E, d = 20_000, 3_000, 200_000, 32
+    pairs = np.stack([rng.integers(0, U, E), rng.integers(0, I, E)], 1)
+
+    class DS:
+        name, n_users, n_items, train_pairs = 'synthetic', U, I, pairs
+
+    def gather_twice(out, t, group=None):
+        out.copy_(torch.cat([t, t]).view(out.shape))
+        return out
+
+    def run(standin):
+        torch.manual_seed(0)
+        m = ShardedIGCN({'embedding_size': d, 'n_layers': 2, 'device': DEV, 'dropout': 0.3, 'feature_ratio': 1.,
+                         'dataset': DS(), 'batch_rep': batch_rep, 'seed': 5}, 0, 1)
+        tr = ShardedIGCNTrainer({'batch_size': 512, 'l2_reg': 1e-4, 'aux_reg': 0.01, 'lr': 1e-2, 'seed': 3}, m)
+        m.world, m.shard.exchange = 2, True
+        monkeypatch.setattr(comm, 'all_reduce_sum', standin)
+        monkeypatch.setattr(comm, 'all_gather_into', gather_twice)
+        m.train()
+        losses = [float(tr.step().detach()) for _ in range(3)]
+        torch.cuda.synchronize()
+        return losses, {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+    want_l, want = run(_sync_standin())
+    got_l, got = run(_standin(torch.cuda.Stream()))
+    assert got_l == want_l and all(np.isfinite(want_l))
+    for k in want:
+        assert torch.equal(got[k], want[k]), k

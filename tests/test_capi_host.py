@@ -217,6 +217,14 @@ def test_new_entry_points_validate_arguments():
              match='NULL')
     _refused('igr_spmm_pull_marked_f32', ctypes.byref(multi.csr), 64, F, F, F, F, 64, F, 1.0, 0, None, F, 64, st,
              match='edge_id')
+    # the shard set-up passes (host memory): sizes, pointers and the output pair are checked
+    n_out = ctypes.c_int64(0)
+    _refused('igr_count_ids', -1, None, 4, None, 0, match='bad args')
+    _refused('igr_count_ids', 3, None, 4, None, 0, match='bad args')
+    _refused('igr_select_id_range', 3, None, None, 0, 2, None, None, ctypes.byref(n_out), 0, match='bad args')
+    keys = np.array([0, 1, 2], np.int64)
+    _refused('igr_select_id_range', 3, keys.ctypes.data, None, 0, 2, keys.ctypes.data, None, ctypes.byref(n_out), 0,
+             match='go together')
     _refused('igr_rowset_mark', 4, F, None, F, st, match='NULL')
     _refused('igr_rowset_sum_f32', 4, 64, F, F, 32, 1.0, F, F, 64, st, match='leading')
     _refused('igr_rowset_sum_f32', 4, 64, None, F, 64, 1.0, F, F, 64, st, match='NULL')

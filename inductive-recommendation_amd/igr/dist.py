@@ -89,6 +89,8 @@ class BipartiteShard:
         self.exchange = world > 1
         if local_pairs is None:
             u, i = (pairs[:, 0], pairs[:, 1]) if isinstance(pairs, np.ndarray) else pairs
+        elif degree is None:
+            raise ValueError('local_pairs needs the degrees of the whole graph (degree=): a range of the pairs cannot give them')
         if degree is None:
             # duplicates count with multiplicity, as scipy sums them into the degree
             degree = np.concatenate([count_ids(u, n_users), count_ids(i, n_items)]).astype(np.float32)

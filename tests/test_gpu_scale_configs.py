@@ -298,6 +298,33 @@ def test_bench_workload_full_size_properties():
     _layer_properties(sh, d)
 
 
+def test_bench_graph_partition_for_8_ranks_full_size():
+    """The 8-GPU configuration's partition at its size (host side only: the shards are built on
+    the CPU, one rank after the other, with the degree all-reduce replaced by the other ranks'
+    counts): eight contiguous user ranges that cover every user, ~50 M edges each (both
+    directions), the same four item row chunks on every rank, all 399,995,952 edges owned once."""
+    from igr import dist
+    from igr.graph import count_ids
+    U, I, W = 10_000_000, 1_000_000, 8
+    u, i = _bench_stream()
+    E = len(u)
+    total = np.concatenate([count_ids(u, U), count_ids(i, I)])
+    nnz, prev, cuts = [], 0, None
+    for r in range(W):
+        e0, e1 = E * r // W, E * (r + 1) // W
+        others = total - np.concatenate([count_ids(u[e0:e1], U), count_ids(i[e0:e1], I)])
+        sh = dist.BipartiteShard.from_stream(u, i, U, I, r, W, 'cpu', reduce=lambda c, o=others: c + o)
+        assert sh.u0 == prev and sh.item_tiles == 1 and sh.user_block.nnz == sh.item_nnz
+        prev = sh.u1
+        c = [(a, b) for a, b, _ in sh.chunks]
+        assert len(c) == 4 and (cuts is None or c == cuts)
+        cuts = c
+        nnz.append(sh.local_nnz)
+        del sh
+    assert prev == U and sum(nnz) == 399_995_952
+    assert max(nnz) - min(nnz) < 1000, nnz  # balanced to within a few users' edges
+
+
 def test_synthetic_d256_full_size_properties():
     """BASELINE configuration 5's layer at its full size: the same 10 M x 1 M x 200 M-draw graph
     at d = 256 (one layer of model.py:4193-4197), which runs as two 128-column passes over

@@ -29,7 +29,9 @@ def main():
     from igr.dist import BipartiteShard
     dev = torch.device('cuda')
     U, I, E, d = 10_000_000, 1_000_000, 200_000_000, args.d
-    pairs = synthetic_pairs(U, I, E, 0)
+    su, si = synthetic_pairs(U, I, E, 0, stacked=False)
+    from igr.graph import count_ids
+    total = np.concatenate([count_ids(su, U), count_ids(si, I)])
     g = torch.Generator(device=dev).manual_seed(2)
     x_items = torch.randn(I, d, generator=g, device=dev) * 0.1
     out = {}
@@ -37,8 +39,10 @@ def main():
         per = []
         for rank in (range(W) if args.ranks == 'all' else [0]):
             t0 = time.time()
-            shard = BipartiteShard(pairs, U, I, rank, W, dev, d=d)
-            shard.world = 1  # compute only: no collective
+            e0, e1 = E * rank // W, E * (rank + 1) // W
+            others = total - np.concatenate([count_ids(su[e0:e1], U), count_ids(si[e0:e1], I)])
+            shard = BipartiteShard.from_stream(su, si, U, I, rank, W, dev, d=d, reduce=lambda c, o=others: c + o)
+            shard.exchange = False  # compute only: no collective
             nu = shard.u1 - shard.u0
             x_users = torch.randn(nu, d, generator=g, device=dev) * 0.1
             y_users = torch.empty(nu, d, device=dev)
